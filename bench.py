@@ -1,0 +1,310 @@
+#!/usr/bin/env python3
+"""Device-resident Internet-checksum throughput on MI355X (BASELINE.json metric).
+
+One "step" = one pass of the hot path over one batch that already sits in
+HBM: a single launch of the engine's span kernel (``uinet_cksum_spans``, the
+C ABI the libuinet shim calls) over the rank's packets, plus -- for N > 1 --
+the one RCCL gather of the 16-bit results to rank 0.  Workload at N = 1 is
+BASELINE.json configs[1] (config 2): 1,048,576 x 1500-B contiguous packets,
+in_cksum_skip(m, 1500, 0).  For N > 1 every rank folds its own 1,048,576
+packets (weak scaling; config 4's 2,097,152 per GPU is ``--packets 2097152``).
+
+Rank 0 prints ONE JSON line.  ``roofline`` prices the span kernel: algorithmic
+bytes per launch (sum of packet lengths) / its mean HIP-event duration on the
+launch stream, against the 8 TB/s HBM3E peak; ``traffic`` is the PMC-measured
+HBM read bytes per launch from profiles/ (FETCH_SIZE x 1024 x 2, the gfx950
+correction of MI355X_MICROARCH.md section HBM) when present for this workload.
+``cpu_baseline`` is the reference's own scalar in_cksum_skip
+(oracle/_ref/libref_cksum.so, compiled from /root/reference) on the same
+bytes laid out as host mbufs, timed on this box's host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=["2", "2rx", "3", "5"], default="2",
+                    help="BASELINE.json config shape (2 = the headline)")
+    ap.add_argument("--packets", type=int, default=None, help="packets per GPU")
+    ap.add_argument("--api", choices=["spans", "strided"], default="spans")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
+                    help="per-launch HBM traffic measured by rocprofv3 --pmc")
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time H2D + kernel + D2H (host-resident rate)")
+    return ap.parse_args()
+
+
+def metric_name() -> str:
+    try:
+        with open(os.path.join(REPO, "BASELINE.json")) as f:
+            return json.load(f)["metric"]
+    except Exception:  # pragma: no cover
+        return "device-resident checksum GiB/s"
+
+
+def build_workload(cfg: str, n, rank: int):
+    import libuinet_amd.workloads as W
+
+    if cfg in ("2", "2rx"):
+        n = n or (1 << 20)
+        w = W.config2_device(n, stride=1514 if cfg == "2rx" else 1500,
+                             base=14 if cfg == "2rx" else 0, rank=rank)
+        w["desc"] = (f"config{cfg}: {n:,} x 1500 B contiguous packets (stride {w['stride']}"
+                     f"{', +14' if cfg == '2rx' else ''}), device-resident, in_cksum_skip(m,1500,0)")
+        w["hint"] = 1500
+    elif cfg == "3":
+        n = n or (1 << 20)
+        w = W.config3_device(n, rank=rank)
+        w["desc"] = (f"config3: {n:,} mixed 64/576/1500 B packets as {w['nseg']:,} chained "
+                     f"1..256 B mbuf segments, in_cksum_skip(m,len,20)")
+        w["hint"] = w["mean_seg"]
+    else:
+        n = n or 131072
+        w = W.config5_device(n, rank=rank)
+        w["desc"] = (f"config5: {n:,} x 9000 B jumbo frames, in_cksum_pseudo_header(m,8980,20,"
+                     f"src,dst,TCP/UDP)")
+        w["hint"] = 8980
+    return w
+
+
+def make_launch(cfg: str, w, api: str, out):
+    import libuinet_amd as u
+
+    if cfg == "3":
+        return lambda s: u.cksum_chains(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"],
+                                        length=w["len"], skip=w["skip"], out=out,
+                                        len_hint=w["hint"], stream=s)
+    if api == "strided" and cfg in ("2", "2rx"):
+        base = w["arena"][w["base"]:]
+        return lambda s: u.cksum_strided(base, w["stride"], w["length"], w["n"], out=out, stream=s)
+    seed = w.get("seed")
+    return lambda s: u.cksum_spans(w["arena"], w["off"], w["len"], seed=seed, out=out,
+                                   len_hint=w["hint"], stream=s)
+
+
+def kernel_name(cfg: str, api: str) -> str:
+    if cfg == "3":
+        return "k_chains"
+    return "k_strided" if api == "strided" else "k_spans"
+
+
+def load_traffic(path: str, key: str):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(key)
+        return None if e is None else float(e["hbm_read_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(cfg: str, w, gpu_out, threads: int):
+    """The reference's scalar in_cksum_skip / in_cksum_pseudo_header over the same
+    bytes as host mbufs; returns the cpu_baseline object (and checks parity)."""
+    import oracle
+    from libuinet_amd.mbuf import MbufChains
+
+    kind = "reference" if oracle.have_reference() else "port"
+    R = oracle.Reference() if kind == "reference" else None
+    host = w["arena"].cpu().numpy()
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        allowed = list(range(os.cpu_count() or 1))
+    threads = max(1, min(threads, len(allowed)))
+    cpus = allowed[:threads]
+    if cfg == "3":
+        lay = w["layout"]
+        ch = MbufChains(host, lay["seg_off"], lay["seg_len"], lay["pkt_seg"])
+        args = (ch.heads, lay["lens"], 20)
+        timer = (lambda nt, cp, r: R.time_skip(*args, nthreads=nt, cpus=cp, reps=r)) if R else None
+        port = lambda: oracle.Oracle().skip_batch(*args, nthreads=threads)  # noqa: E731
+    elif cfg == "5":
+        ch = MbufChains.contiguous(host, w["frame"] * np.arange(w["n"], dtype=np.int64), w["frame"])
+        args = (ch.heads, w["plen"], w["off0"], w["src"], w["dst"], w["proto"])
+        timer = (lambda nt, cp, r: R.time_pseudo(*args, nthreads=nt, cpus=cp, reps=r)) if R else None
+        port = lambda: oracle.Oracle().pseudo_header_batch(*args)  # noqa: E731
+    else:
+        off = w["off"].cpu().numpy()
+        ch = MbufChains.contiguous(host, off, w["length"])
+        args = (ch.heads, w["length"], 0)
+        timer = (lambda nt, cp, r: R.time_skip(*args, nthreads=nt, cpus=cp, reps=r)) if R else None
+        port = lambda: oracle.Oracle().skip_batch(*args, nthreads=threads)  # noqa: E731
+    gib = w["bytes"] / 2**30
+    if timer is not None:
+        t1, out1 = timer(1, cpus[:1], 3)
+        tn, outn = timer(threads, cpus, 5)
+    else:  # oracle restatement, timed the same way
+        t0 = time.perf_counter(); out1 = port(); t1 = time.perf_counter() - t0  # noqa: E702
+        tn, outn = t1, out1
+        threads = threads
+    parity = bool(np.array_equal(outn, gpu_out) and np.array_equal(out1, gpu_out))
+    return {
+        "value": round(gib / tn, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "sample": (f"{w['n']:,} packets ({gib:.3f} GiB algorithmic) of the benchmarked batch, "
+                   f"host copy as {'chained ' if cfg == '3' else ''}struct mbuf; best of 5 on "
+                   f"{threads} pinned threads; 1 thread: {gib / t1:.3f} GiB/s best of 3; "
+                   f"results bit-identical to the GPU: {parity}"),
+        "one_thread_gibs": round(gib / t1, 3),
+        "bit_identical_to_gpu": parity,
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import libuinet_amd as u
+    from libuinet_amd.dist import gather_results
+
+    if not u.device_ok():
+        raise SystemExit("bench: no gfx950 device visible")
+    w = build_workload(args.config, args.packets, rank)
+    n = w["n"]
+    out = torch.empty(n, dtype=torch.uint16, device="cuda")
+    stream = torch.cuda.current_stream()
+    launch = make_launch(args.config, w, args.api, out)
+    counts = [n] * world
+    K, Wm = args.steps, args.warmup
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
+
+    def step(k=None):
+        if k is not None:
+            ev[k][0].record(stream)
+        launch(stream)
+        if k is not None:
+            ev[k][1].record(stream)
+        if world > 1:
+            gather_results(out, counts)
+
+    for _ in range(Wm):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kms = np.array([a.elapsed_time(b) for a, b in ev])  # ms, kernel only
+
+    result = None
+    if rank == 0:
+        total_bytes = w["bytes"] * world * K
+        value = total_bytes / elapsed / 2**30
+        achieved = w["bytes"] / (kms.mean() * 1e-3) / 1e9
+        key = f"{kernel_name(args.config, args.api)}:config{args.config}:{n}"
+        traffic = load_traffic(args.pmc, key)
+        result = {
+            "metric": metric_name(),
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": Wm,
+            "ms_per_step": round(elapsed / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16 one's-complement (u32 loads, u64 accumulate)",
+            "data": "synthetic (splitmix64 payload, BASELINE.md seeds)",
+            "config": {
+                "workload": w["desc"],
+                "packets_per_gpu": n,
+                "algorithmic_bytes_per_gpu": w["bytes"],
+                "api": {"spans": "uinet_cksum_spans", "strided": "uinet_cksum_strided"}[args.api]
+                if args.config != "3" else "uinet_cksum_chains",
+                "parallelism": f"dp{world} packet shards" + (" + RCCL gather of u16 results"
+                                                             if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": kernel_name(args.config, args.api),
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": w["bytes"],
+                "kernel_ms_mean": round(float(kms.mean()), 5),
+                "kernel_ms_min": round(float(kms.min()), 5),
+            },
+        }
+        if args.host_path:
+            result["host_resident"] = host_path_rate(args, w)
+    if world == 1 and rank == 0 and args.cpu_baseline == "auto":
+        torch.cuda.synchronize()
+        gpu_out = out.cpu().view(torch.int16).numpy().view(np.uint16)
+        result["cpu_baseline"] = cpu_baseline(args.config, w, gpu_out, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def host_path_rate(args, w):
+    """H2D of the whole batch from pinned host memory + kernel + D2H of the
+    results (the rate when packets start and end in host memory)."""
+    import torch
+    import libuinet_amd as u
+
+    if args.config not in ("2", "2rx", "5"):
+        return None
+    host = w["arena"].cpu().pin_memory()
+    dev = torch.empty_like(w["arena"])
+    res = torch.empty(w["n"], dtype=torch.uint16).pin_memory()
+    out = torch.empty(w["n"], dtype=torch.uint16, device="cuda")
+    s = torch.cuda.current_stream()
+    best = 1e30
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev.copy_(host, non_blocking=True)
+        u.cksum_spans(dev, w["off"], w["len"], seed=w.get("seed"), out=out, len_hint=w["hint"],
+                      stream=s)
+        res.copy_(out, non_blocking=True)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    return {"gibs": round(w["bytes"] / best / 2**30, 3), "ms": round(best * 1e3, 3),
+            "what": "pinned host arena -> HBM copy + span kernel + u16 results -> pinned host"}
+
+
+if __name__ == "__main__":
+    main()

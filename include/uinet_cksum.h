@@ -1,0 +1,169 @@
+/*
+ * uinet_cksum.h -- C ABI of the MI355X Internet-checksum engine.
+ *
+ * Two layers:
+ *
+ *  1. The drop-in per-call ABI of libuinet's checksum KPI, with the exact
+ *     signatures of /root/reference/sys/amd64/include/in_cksum.h:44,76-83 (the
+ *     object the amd64 build compiles, sys/amd64/amd64/in_cksum.c).  Linking
+ *     libuinet_cksum in place of that object keeps lib/libuinet and
+ *     bin/multitool unchanged.  The data-touching entry points
+ *     run on the GPU (a batch of one, synchronous).
+ *
+ *  2. Batch entry points for callers that hold many packets at once
+ *     (the RX/TX driver batches of SURVEY.md section 8f), and the
+ *     device-resident descriptor API that is the hot path proper: one HIP
+ *     launch folds a whole batch of packets that already sit in HBM.
+ *
+ * Results are bit-identical to the reference on the same inputs.  Nothing
+ * here silently falls back to a CPU computation: the batch and device entry
+ * points return a negative UINET_CKSUM_E* code, the per-call ABI (which has no
+ * error channel, like the reference) prints the HIP error and aborts.
+ */
+#ifndef UINET_CKSUM_H
+#define UINET_CKSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The library is built with -fvisibility=hidden: exactly the functions
+ * declared below are exported. */
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
+/* libuinet's struct mbuf (sys/sys/mbuf.h:153-171).  Only m_next (offset 0),
+ * m_data (offset 16) and m_len (int, offset 24) are read; the chain is
+ * borrowed read-only, never modified, freed or pulled up. */
+struct mbuf;
+/* struct ip (sys/netinet/ip.h:49-70): 20 bytes, ip_sum at offset 10. */
+struct ip;
+
+/* ------------------------------------------------------------------------ */
+/* 1. Drop-in per-call ABI (sys/amd64/include/in_cksum.h)                    */
+/* ------------------------------------------------------------------------ */
+
+#ifndef in_cksum
+/* in_cksum.h:44 -- there is no in_cksum symbol on amd64. */
+#define in_cksum(m, len) in_cksum_skip(m, len, 0)
+#endif
+
+/* in_cksum.h:83, in_cksum.c:193-232.  Sums bytes [skip, len) of the chain
+ * (len counts from the chain start), returns the complemented 16-bit sum. */
+unsigned short in_cksum_skip(struct mbuf *m, int len, int skip);
+
+/* in_cksum.h:78-79, in_cksum.c:241-276.  Pseudo-header seed
+ * src + dst + htons(proto) + htons(plen), then plen bytes from off0 in the
+ * first mbuf onward.  0 means "valid" on receive. */
+uint16_t in_cksum_pseudo_header(struct mbuf *m, int plen, int off0,
+    uint32_t src, uint32_t dst, uint8_t protonum);
+
+/* in_cksum.h:77, in_cksum.c:278-285.  20-byte IPv4 header, complemented. */
+unsigned int in_cksum_hdr(const struct ip *ip);
+
+/* in_cksum.h:82, in_cksum.c:181-191.  Folded, NOT complemented. */
+unsigned short in_pseudo(unsigned int a, unsigned int b, unsigned int c);
+
+/* in_cksum.h:81, in_cksum.c:172-179.  a + b with one end-around carry. */
+unsigned short in_addword(unsigned short a, unsigned short b);
+
+/* in_cksum.h:55-61: incremental TTL-decrement update of ip_sum, on the raw
+ * header bytes (ip_sum is the big-endian 16-bit field at offset 10). */
+static inline void
+uinet_in_cksum_update(void *ip_hdr)
+{
+	unsigned char *p = (unsigned char *)ip_hdr + 10;
+	int s = (int)(((unsigned)p[0] << 8) | p[1]) + 256;
+
+	s = s + (s >> 16);
+	p[0] = (unsigned char)(s >> 8);
+	p[1] = (unsigned char)s;
+}
+
+/* ------------------------------------------------------------------------ */
+/* 2a. Status                                                                */
+/* ------------------------------------------------------------------------ */
+
+#define UINET_CKSUM_OK       0
+#define UINET_CKSUM_EINVAL (-22) /* bad argument                        */
+#define UINET_CKSUM_ENODEV (-19) /* no usable gfx950 device             */
+#define UINET_CKSUM_ENOMEM (-12) /* host or device allocation failed    */
+#define UINET_CKSUM_EHIP   (-5)  /* HIP runtime error; see last_hip_error */
+
+/* Result flags for the batch/device entry points. */
+#define UINET_CKSUM_F_UDP           0x1u /* 0 -> 0xffff (ip_output.c:962-963) */
+#define UINET_CKSUM_F_NO_COMPLEMENT 0x2u /* return the folded sum, in_pseudo-style */
+
+/* Engine version string and HIP diagnostics. */
+const char *uinet_cksum_version(void);
+const char *uinet_cksum_strerror(int code);
+int uinet_cksum_last_hip_error(void);
+/* 1 when a gfx950 device is visible to the calling thread, else 0. */
+int uinet_cksum_device_ok(void);
+
+/* ------------------------------------------------------------------------ */
+/* 2b. Device-resident descriptor API (the hot path)                         */
+/*                                                                          */
+/* All array pointers are device pointers (HBM).  Launches are asynchronous  */
+/* on `stream` (a hipStream_t; NULL = the legacy default stream).  A         */
+/* `len_hint` (mean bytes per packet, 0 = unknown) selects the lanes-per-    */
+/* packet geometry; it never changes results.                                */
+/* ------------------------------------------------------------------------ */
+
+/* One contiguous span per packet:
+ *   out[i] = checksum of bytes [base + off[i], base + off[i] + len[i])
+ * where the span's first byte sits at logical parity parity[i] & 1
+ * (parity NULL = all 0, the in_cksum_skip case) and seed[i] (NULL = 0) is
+ * added before folding (the in_cksum_pseudo_header seed). */
+int uinet_cksum_spans(const void *base, const uint64_t *off,
+    const uint32_t *len, const uint32_t *seed, const uint8_t *parity,
+    uint16_t *out, uint32_t n, uint32_t flags, uint32_t len_hint,
+    void *stream);
+
+/* Same, for the fixed-geometry batch "packet i starts at base + i * stride
+ * and is len bytes long" (no descriptor arrays are read). */
+int uinet_cksum_strided(const void *base, uint64_t stride, uint32_t len,
+    const uint32_t *seed, uint16_t *out, uint32_t n, uint32_t flags,
+    void *stream);
+
+/* Chained packets (device-resident mbuf chains resolved to segments):
+ * packet i is the chain of segments [pkt_seg[i], pkt_seg[i + 1]), segment k
+ * being the device bytes [base + seg_off[k], + seg_len[k]).  out[i] is
+ * in_cksum_skip(chain_i, len[i], skip[i]) exactly as in_cksum.c:193-232
+ * defines it (len counts from the chain start; len NULL = whole chain, skip
+ * NULL = 0), plus seed[i] (NULL = 0) before folding.  `len_hint` is the mean
+ * SEGMENT length here. */
+int uinet_cksum_chains(const void *base, const uint64_t *seg_off,
+    const uint32_t *seg_len, const uint32_t *pkt_seg, const uint32_t *len,
+    const uint32_t *skip, const uint32_t *seed, uint16_t *out, uint32_t n,
+    uint32_t flags, uint32_t len_hint, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* 2c. Host-mbuf batch API (synchronous; for the driver RX/TX batch hooks)   */
+/*                                                                          */
+/* The chains are walked on the host exactly as the per-call functions walk  */
+/* them, the bytes are staged through pinned memory to HBM, one launch folds */
+/* the batch, and the results are copied back.  Thread-safe: every calling   */
+/* thread owns its own stream and staging.                                   */
+/* ------------------------------------------------------------------------ */
+
+int in_cksum_skip_batch(struct mbuf *const *m, const int *len,
+    const int *skip, unsigned short *out, int n);
+int in_cksum_pseudo_header_batch(struct mbuf *const *m, const int *plen,
+    const int *off0, const uint32_t *src, const uint32_t *dst,
+    const uint8_t *protonum, uint16_t *out, int n);
+int in_cksum_hdr_batch(const struct ip *const *ip, unsigned int *out, int n);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UINET_CKSUM_H */

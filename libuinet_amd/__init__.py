@@ -1,0 +1,275 @@
+"""libuinet_amd -- MI355X-native engine for libuinet's Internet checksum.
+
+Python mirror of the engine's C ABI (``include/uinet_cksum.h``), which keeps
+the reference KPI of /root/reference/sys/amd64/include/in_cksum.h:44,76-83:
+
+* per-call, same names and argument meaning as the reference:
+  :func:`in_cksum_skip`, :func:`in_cksum` (macro), :func:`in_cksum_pseudo_header`,
+  :func:`in_cksum_hdr`, :func:`in_pseudo`, :func:`in_addword`;
+* host-mbuf batches: :func:`in_cksum_skip_batch`, :func:`in_cksum_pseudo_header_batch`,
+  :func:`in_cksum_hdr_batch`;
+* the device-resident hot path over HBM buffers held in torch tensors:
+  :func:`cksum_spans`, :func:`cksum_strided`, :func:`cksum_chains`.
+
+Everything that touches packet bytes runs in the HIP library
+``libuinet_amd/libuinet_cksum.so``; if it is missing or no gfx950 device is
+usable the calls raise -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+from .mbuf import MBUF_DTYPE, MSIZE, MbufChains, SEED_BASE, aligned_empty, splitmix64_bytes
+
+__all__ = [
+    "LIB_PATH", "CksumError", "lib", "in_cksum", "in_cksum_skip", "in_cksum_pseudo_header",
+    "in_cksum_hdr", "in_pseudo", "in_addword", "in_cksum_skip_batch",
+    "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch", "cksum_spans", "cksum_strided",
+    "cksum_chains", "F_UDP", "F_NO_COMPLEMENT", "MbufChains", "MBUF_DTYPE", "MSIZE",
+    "SEED_BASE", "aligned_empty", "splitmix64_bytes", "EXPORTED_SYMBOLS",
+]
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libuinet_cksum.so")
+
+F_UDP = 0x1
+F_NO_COMPLEMENT = 0x2
+
+OK, EINVAL, ENODEV, ENOMEM, EHIP = 0, -22, -19, -12, -5
+
+# Every function include/uinet_cksum.h declares (tests check the .so exports
+# exactly these).
+EXPORTED_SYMBOLS = (
+    "in_cksum_skip", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo", "in_addword",
+    "uinet_cksum_version", "uinet_cksum_strerror", "uinet_cksum_last_hip_error",
+    "uinet_cksum_device_ok", "uinet_cksum_spans", "uinet_cksum_strided", "uinet_cksum_chains",
+    "in_cksum_skip_batch", "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch",
+)
+
+
+class CksumError(RuntimeError):
+    """A negative UINET_CKSUM_E* status from the engine."""
+
+    def __init__(self, fn: str, code: int):
+        self.code = code
+        msg = lib().uinet_cksum_strerror(code).decode()
+        hip = lib().uinet_cksum_last_hip_error()
+        super().__init__(f"{fn}: {msg} (code {code}, hip error {hip})")
+
+
+_LIB: Optional[ctypes.CDLL] = None
+
+_vp, _u64, _u32, _i32, _u16, _u8 = (ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                    ctypes.c_int, ctypes.c_uint16, ctypes.c_uint8)
+
+
+def lib() -> ctypes.CDLL:
+    """Load the engine library (torch first, so both share one HIP runtime:
+    torch's bundled libamdhip64 and ROCm's carry the same SONAME)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - torch is part of the image
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is not built; run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "in_cksum_skip": (ctypes.c_ushort, [_vp, _i32, _i32]),
+        "in_cksum_pseudo_header": (_u16, [_vp, _i32, _i32, _u32, _u32, _u8]),
+        "in_cksum_hdr": (ctypes.c_uint, [_vp]),
+        "in_pseudo": (ctypes.c_ushort, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]),
+        "in_addword": (ctypes.c_ushort, [ctypes.c_ushort, ctypes.c_ushort]),
+        "uinet_cksum_version": (ctypes.c_char_p, []),
+        "uinet_cksum_strerror": (ctypes.c_char_p, [_i32]),
+        "uinet_cksum_last_hip_error": (_i32, []),
+        "uinet_cksum_device_ok": (_i32, []),
+        "uinet_cksum_spans": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]),
+        "uinet_cksum_strided": (_i32, [_vp, _u64, _u32, _vp, _vp, _u32, _u32, _vp]),
+        "uinet_cksum_chains": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32,
+                                       _vp]),
+        "in_cksum_skip_batch": (_i32, [_vp, _vp, _vp, _vp, _i32]),
+        "in_cksum_pseudo_header_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32]),
+        "in_cksum_hdr_batch": (_i32, [_vp, _vp, _i32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def _check(fn: str, rc: int) -> None:
+    if rc != OK:
+        raise CksumError(fn, rc)
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# ---- per-call ABI (sys/amd64/include/in_cksum.h) ----------------------------
+
+def in_cksum_skip(m: int, len: int, skip: int) -> int:  # noqa: A002 - reference name
+    """in_cksum.c:193-232.  ``m`` is the address of a ``struct mbuf``."""
+    return lib().in_cksum_skip(m, len, skip)
+
+
+def in_cksum(m: int, len: int) -> int:  # noqa: A002
+    """in_cksum.h:44 -- ``in_cksum_skip(m, len, 0)``."""
+    return lib().in_cksum_skip(m, len, 0)
+
+
+def in_cksum_pseudo_header(m: int, plen: int, off0: int, src: int, dst: int, protonum: int) -> int:
+    """in_cksum.c:241-276; ``src``/``dst`` as stored in the header (network
+    order read as a native u32)."""
+    return lib().in_cksum_pseudo_header(m, plen, off0, src, dst, protonum)
+
+
+def in_cksum_hdr(ip: int) -> int:
+    """in_cksum.c:278-285.  ``ip`` is the address of the 20-byte header."""
+    return lib().in_cksum_hdr(ip)
+
+
+def in_pseudo(a: int, b: int, c: int) -> int:
+    """in_cksum.c:181-191 (folded, not complemented)."""
+    return lib().in_pseudo(a, b, c)
+
+
+def in_addword(a: int, b: int) -> int:
+    """in_cksum.c:172-179."""
+    return lib().in_addword(a, b)
+
+
+# ---- host-mbuf batches --------------------------------------------------------
+
+def in_cksum_skip_batch(heads, length, skip) -> np.ndarray:
+    heads = np.ascontiguousarray(heads, dtype=np.uint64)
+    n = heads.size
+    length = np.ascontiguousarray(np.broadcast_to(length, (n,)), dtype=np.int32)
+    skip = np.ascontiguousarray(np.broadcast_to(skip, (n,)), dtype=np.int32)
+    out = np.zeros(n, dtype=np.uint16)
+    _check("in_cksum_skip_batch",
+           lib().in_cksum_skip_batch(_ptr(heads), _ptr(length), _ptr(skip), _ptr(out), n))
+    return out
+
+
+def in_cksum_pseudo_header_batch(heads, plen, off0, src, dst, proto) -> np.ndarray:
+    heads = np.ascontiguousarray(heads, dtype=np.uint64)
+    n = heads.size
+    arrs = [np.ascontiguousarray(np.broadcast_to(a, (n,)), dtype=t)
+            for a, t in ((plen, np.int32), (off0, np.int32), (src, np.uint32),
+                         (dst, np.uint32), (proto, np.uint8))]
+    out = np.zeros(n, dtype=np.uint16)
+    _check("in_cksum_pseudo_header_batch",
+           lib().in_cksum_pseudo_header_batch(_ptr(heads), *[_ptr(a) for a in arrs], _ptr(out), n))
+    return out
+
+
+def in_cksum_hdr_batch(ips) -> np.ndarray:
+    ips = np.ascontiguousarray(ips, dtype=np.uint64)
+    out = np.zeros(ips.size, dtype=np.uint32)
+    _check("in_cksum_hdr_batch", lib().in_cksum_hdr_batch(_ptr(ips), _ptr(out), ips.size))
+    return out
+
+
+# ---- device-resident hot path (torch tensors in HBM) -------------------------
+
+def _dev(t, dtype, name):
+    import torch
+
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a device tensor")
+    if t.dtype != dtype or not t.is_contiguous():
+        raise TypeError(f"{name} must be a contiguous {dtype} tensor")
+    return t
+
+
+def _dp(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _stream(stream) -> int:
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def _out(n, out, like):
+    import torch
+
+    if out is None:
+        return torch.empty(n, dtype=torch.uint16, device=like.device)
+    return _dev(out, torch.uint16, "out")
+
+
+def cksum_spans(base, off, length, seed=None, parity=None, out=None, flags: int = 0,
+                len_hint: int = 0, stream=None):
+    """out[i] = checksum of ``base[off[i] : off[i] + length[i]]`` (device u8 tensor
+    ``base``; int64 ``off``; int32 ``length``; optional uint32-valued int32
+    ``seed``; optional uint8 ``parity``)."""
+    import torch
+
+    _dev(base, torch.uint8, "base")
+    _dev(off, torch.int64, "off")
+    _dev(length, torch.int32, "length")
+    _dev(seed, torch.int32, "seed")
+    _dev(parity, torch.uint8, "parity")
+    n = off.numel()
+    if length.numel() != n:
+        raise ValueError("off/length size mismatch")
+    out = _out(n, out, base)
+    _check("uinet_cksum_spans", lib().uinet_cksum_spans(
+        _dp(base), _dp(off), _dp(length), _dp(seed), _dp(parity), _dp(out), n, flags,
+        len_hint, _stream(stream)))
+    return out
+
+
+def cksum_strided(base, stride: int, length: int, n: int, seed=None, out=None,
+                  flags: int = 0, stream=None):
+    """out[i] = checksum of ``base[i*stride : i*stride + length]``."""
+    import torch
+
+    _dev(base, torch.uint8, "base")
+    _dev(seed, torch.int32, "seed")
+    if n and (n - 1) * stride + length > base.numel():
+        raise ValueError("strided batch exceeds base")
+    out = _out(n, out, base)
+    _check("uinet_cksum_strided", lib().uinet_cksum_strided(
+        _dp(base), stride, length, _dp(seed), _dp(out), n, flags, _stream(stream)))
+    return out
+
+
+def cksum_chains(base, seg_off, seg_len, pkt_seg, length=None, skip=None, seed=None, out=None,
+                 flags: int = 0, len_hint: int = 0, stream=None):
+    """``in_cksum_skip(chain_i, length[i], skip[i])`` for device-resident chains:
+    packet i = segments [pkt_seg[i], pkt_seg[i+1]) of ``base`` (int64 seg_off,
+    int32 seg_len, int32 pkt_seg of n+1 entries; optional int32 length/skip/seed)."""
+    import torch
+
+    _dev(base, torch.uint8, "base")
+    _dev(seg_off, torch.int64, "seg_off")
+    _dev(seg_len, torch.int32, "seg_len")
+    _dev(pkt_seg, torch.int32, "pkt_seg")
+    for t, nm in ((length, "length"), (skip, "skip"), (seed, "seed")):
+        _dev(t, torch.int32, nm)
+    n = pkt_seg.numel() - 1
+    out = _out(n, out, base)
+    _check("uinet_cksum_chains", lib().uinet_cksum_chains(
+        _dp(base), _dp(seg_off), _dp(seg_len), _dp(pkt_seg), _dp(length), _dp(skip), _dp(seed),
+        _dp(out), n, flags, len_hint, _stream(stream)))
+    return out
+
+
+def device_ok() -> bool:
+    return bool(lib().uinet_cksum_device_ok())

@@ -1,0 +1,27 @@
+// Internal interfaces between the HIP kernels (cksum_kernels.hip) and the
+// host side of the engine (cksum_api.hip).  Not part of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "uinet_cksum.h"
+
+namespace uinet {
+
+// Records the HIP error (if any) of the last launch on this thread and maps
+// it to a UINET_CKSUM_* code.
+int check_launch();
+int record_hip(hipError_t e);
+
+int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
+                 const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                 uint32_t flags, uint32_t len_hint, hipStream_t stream);
+int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const uint32_t* seed,
+                   uint16_t* out, uint32_t n, uint32_t flags, hipStream_t stream);
+int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
+                  const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
+                  const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                  uint32_t len_hint, hipStream_t stream);
+
+}  // namespace uinet

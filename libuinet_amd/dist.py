@@ -1,0 +1,58 @@
+"""Multi-GPU sharding of packet batches (one process per GPU).
+
+The checksum has no cross-packet term, so a batch is cut into
+contiguous packet ranges -- balanced by bytes when lengths vary -- every rank
+folds its range on its own GPU with no data-path collective, and the one
+exchange step is a single gather of the 16-bit results to the root over RCCL
+(torch.distributed "nccl" is RCCL on ROCm; gloo on CPU in the tests).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_bounds(n: int, world: int, weights=None) -> np.ndarray:
+    """Packet-index bounds ``b`` (world + 1 entries) so rank r owns
+    ``[b[r], b[r+1])``: equal counts, or equal ``weights`` (bytes) sums."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    if weights is None:
+        return (np.arange(world + 1, dtype=np.int64) * n) // world
+    w = np.asarray(weights, dtype=np.float64)
+    if w.size != n:
+        raise ValueError("weights must have one entry per packet")
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    targets = cum[-1] * np.arange(world + 1) / world
+    b = np.searchsorted(cum, targets, side="left").astype(np.int64)
+    b[0], b[-1] = 0, n
+    return np.maximum.accumulate(b)
+
+
+def shard_range(n: int, rank: int, world: int, weights=None) -> tuple[int, int]:
+    b = shard_bounds(n, world, weights)
+    return int(b[rank]), int(b[rank + 1])
+
+
+def gather_results(local, counts, group=None, dst: int = 0):
+    """Gather every rank's 16-bit results (``local``: 1-D uint16/int16 tensor,
+    ``counts[r]`` entries on rank r) into one tensor on ``dst`` with one
+    collective; other ranks get None.  Ranks with fewer packets are padded
+    to the largest shard so the collective moves equal-sized buffers."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    cmax = 2 * int(max(counts))
+    # Moved as bytes: every backend (gloo, RCCL) carries uint8.
+    send = local.contiguous().view(torch.uint8)
+    if send.numel() < cmax:
+        pad = torch.zeros(cmax, dtype=torch.uint8, device=send.device)
+        pad[: send.numel()] = send
+        send = pad
+    gl = [torch.empty(cmax, dtype=torch.uint8, device=send.device) for _ in range(world)] \
+        if rank == dst else None
+    dist.gather(send, gather_list=gl, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([g[: 2 * int(c)] for g, c in zip(gl, counts)]).view(local.dtype)

@@ -1,0 +1,349 @@
+"""GPU parity: every entry point of the HIP engine, bit-exact against the
+oracle (itself pinned to the reference's golden vectors) and against the
+golden vectors directly.  Runs on an MI355X (`pytest -m gpu`)."""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import pytest
+
+import libuinet_amd as u
+from libuinet_amd.mbuf import MbufChains, aligned_empty, splitmix64_bytes
+
+from test_oracle import pcap_cases
+
+pytestmark = pytest.mark.gpu
+
+HINTS = (0, 64, 200, 500, 1500, 9000)  # every kernel geometry
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert u.device_ok(), "device is not gfx950"
+    return torch
+
+
+def dev(torch, a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def host16(t) -> np.ndarray:
+    return t.cpu().view(__import__("torch").int16).numpy().view(np.uint16)
+
+
+def rand_arena(nbytes: int, seed: int) -> np.ndarray:
+    a = aligned_empty(nbytes)
+    splitmix64_bytes(nbytes, seed, out=a)
+    return a
+
+
+def rand_spans(rng, n, arena_size, max_len):
+    ln = rng.integers(0, max_len + 1, n)
+    edge = rng.random(n)
+    ln = np.where(edge < 0.05, rng.choice([0, 1, 2, 3, 4, 15, 16, 17, 31, 32, 33], n), ln)
+    off = rng.integers(0, arena_size - max_len - 1, n)
+    return off.astype(np.int64), ln.astype(np.int64)
+
+
+# ---- device-resident API ------------------------------------------------------
+
+@pytest.mark.parametrize("hint", HINTS)
+@pytest.mark.parametrize("flags", [0, u.F_UDP, u.F_NO_COMPLEMENT])
+def test_spans_random(torch_dev, ora, hint, flags):
+    torch = torch_dev
+    rng = np.random.default_rng(hint * 7 + flags)
+    arena = rand_arena(1 << 21, 17 + hint)
+    n = 6000
+    off, ln = rand_spans(rng, n, arena.size, 3000)
+    seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    seed[rng.random(n) < 0.3] = 0
+    par = rng.integers(0, 2, n).astype(np.uint8)
+    want = ora.spans(arena, off, ln, seed, par, flags)
+    got = u.cksum_spans(dev(torch, arena), dev(torch, off), dev(torch, ln.astype(np.int32)),
+                        seed=dev(torch, seed.view(np.int32)), parity=dev(torch, par),
+                        flags=flags, len_hint=hint)
+    np.testing.assert_array_equal(host16(got), want)
+
+
+@pytest.mark.parametrize("hint", HINTS)
+def test_spans_no_seed_no_parity(torch_dev, ora, hint):
+    torch = torch_dev
+    rng = np.random.default_rng(99 + hint)
+    arena = rand_arena(1 << 20, 5)
+    off, ln = rand_spans(rng, 4000, arena.size, 1600)
+    want = ora.spans(arena, off, ln)
+    got = u.cksum_spans(dev(torch, arena), dev(torch, off), dev(torch, ln.astype(np.int32)),
+                        len_hint=hint)
+    np.testing.assert_array_equal(host16(got), want)
+
+
+def test_spans_long(torch_dev, ora):
+    """Spans far longer than one unrolled round of any geometry."""
+    torch = torch_dev
+    arena = rand_arena(40 << 20, 23)
+    off = np.array([0, 1, 3, 4097, 5 << 20, 7], np.int64)
+    ln = np.array([1 << 16, (1 << 20) + 3, 9000, 65535, 32 << 20, 0], np.int64)
+    want = ora.spans(arena, off, ln)
+    for hint in HINTS:
+        got = u.cksum_spans(dev(torch, arena), dev(torch, off), dev(torch, ln.astype(np.int32)),
+                            len_hint=hint)
+        np.testing.assert_array_equal(host16(got), want)
+
+
+def test_spans_zero_and_ff(torch_dev, ora):
+    torch = torch_dev
+    for fill in (0x00, 0xFF):
+        arena = aligned_empty(1 << 16)
+        arena[:] = fill
+        off = np.arange(0, 64 * 17, 17, dtype=np.int64)
+        ln = np.arange(64, dtype=np.int64) * 13
+        want = ora.spans(arena, off, ln)
+        got = u.cksum_spans(dev(torch, arena), dev(torch, off), dev(torch, ln.astype(np.int32)))
+        np.testing.assert_array_equal(host16(got), want)
+        if fill == 0:
+            assert (want == 0xFFFF).all()
+
+
+def test_empty_batch(torch_dev):
+    torch = torch_dev
+    arena = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    e64 = torch.zeros(0, dtype=torch.int64, device="cuda")
+    e32 = torch.zeros(0, dtype=torch.int32, device="cuda")
+    assert u.cksum_spans(arena, e64, e32).numel() == 0
+    assert u.cksum_strided(arena, 16, 16, 0).numel() == 0
+
+
+@pytest.mark.parametrize("stride,length,base", [(1500, 1500, 0), (1514, 1500, 14), (9000, 9000, 0),
+                                                (1501, 1500, 1), (64, 64, 0), (600, 576, 3)])
+def test_strided(torch_dev, ora, stride, length, base):
+    torch = torch_dev
+    n = 3000
+    arena = rand_arena(base + stride * n + 64, stride)
+    off = base + stride * np.arange(n, dtype=np.int64)
+    want = ora.spans(arena, off, length)
+    d = dev(torch, arena)
+    got = u.cksum_strided(d[base:], stride, length, n)
+    np.testing.assert_array_equal(host16(got), want)
+
+
+def random_chain_layout(rng, n, arena_size, max_seg=256, max_segs=8):
+    nseg = rng.integers(1, max_segs + 1, n)
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = rng.integers(1, max_seg + 1, s)
+    seg_len[rng.random(s) < 0.08] = 0
+    seg_off = rng.integers(0, arena_size - max_seg - 1, s)
+    return seg_off.astype(np.int64), seg_len.astype(np.int64), pkt_seg
+
+
+@pytest.mark.parametrize("hint", HINTS)
+def test_chains_random(torch_dev, ora, hint):
+    torch = torch_dev
+    rng = np.random.default_rng(1000 + hint)
+    arena = rand_arena(1 << 20, 31)
+    seg_off, seg_len, pkt_seg = random_chain_layout(rng, 5000, arena.size,
+                                                   max_seg=max(hint, 64) if hint else 256)
+    seed = rng.integers(0, 2**32, pkt_seg.size - 1, dtype=np.uint64).astype(np.uint32)
+    want = ora.chains(arena, seg_off, seg_len, pkt_seg, seed=seed)
+    got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
+                         dev(torch, pkt_seg.astype(np.int32)), seed=dev(torch, seed.view(np.int32)),
+                         len_hint=hint)
+    np.testing.assert_array_equal(host16(got), want)
+    # and the same chains as host mbufs through the reference-shaped walk
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1])
+    np.testing.assert_array_equal(ora.chains(arena, seg_off, seg_len, pkt_seg),
+                                  ora.skip_batch(ch.heads, tot, 0))
+
+
+# ---- host-mbuf batch API and the per-call drop-in ABI -------------------------
+
+def test_golden_skip_batch(torch_dev, arena, golden):
+    g = golden("skip")
+    ch = MbufChains(arena, g["seg_off"], g["seg_len"], g["pkt_seg"])
+    np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, g["len"], g["skip"]), g["expected"])
+
+
+def test_golden_skip_per_call(torch_dev, arena, golden):
+    g = golden("skip")
+    ch = MbufChains(arena, g["seg_off"], g["seg_len"], g["pkt_seg"])
+    for i in range(0, ch.n, 11):
+        assert u.in_cksum_skip(ch.head(i), int(g["len"][i]), int(g["skip"][i])) == g["expected"][i]
+        if g["skip"][i] == 0:
+            assert u.in_cksum(ch.head(i), int(g["len"][i])) == g["expected"][i]
+
+
+def test_golden_pseudo_batch(torch_dev, arena, golden):
+    g = golden("pseudo")
+    ch = MbufChains(arena, g["seg_off"], g["seg_len"], g["pkt_seg"])
+    got = u.in_cksum_pseudo_header_batch(ch.heads, g["plen"], g["off0"], g["src"], g["dst"], g["proto"])
+    np.testing.assert_array_equal(got, g["expected"])
+    for i in range(0, ch.n, 23):
+        assert u.in_cksum_pseudo_header(ch.head(i), int(g["plen"][i]), int(g["off0"][i]),
+                                        int(g["src"][i]), int(g["dst"][i]),
+                                        int(g["proto"][i])) == g["expected"][i]
+
+
+def test_golden_hdr_batch(torch_dev, arena, golden):
+    g = golden("hdr")
+    ips = arena.ctypes.data + g["off"].astype(np.uint64)
+    np.testing.assert_array_equal(u.in_cksum_hdr_batch(ips), g["expected"])
+    for i in range(0, ips.size, 17):
+        assert u.in_cksum_hdr(int(ips[i])) == g["expected"][i]
+
+
+def test_golden_configs(torch_dev, arena, golden):
+    torch = torch_dev
+    g = golden("configs")
+    d = dev(torch, arena)
+    for tag in ("c2", "c2rx"):
+        ch = MbufChains.contiguous(arena, g[f"{tag}_off"], 1500)
+        np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, 1500, 0), g[f"{tag}_expected"])
+        got = u.cksum_spans(d, dev(torch, g[f"{tag}_off"]),
+                            dev(torch, np.full(64, 1500, np.int32)), len_hint=1500)
+        np.testing.assert_array_equal(host16(got), g[f"{tag}_expected"])
+    ch = MbufChains(arena, g["c3_seg_off"], g["c3_seg_len"], g["c3_pkt_seg"])
+    np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, g["c3_len"], 20), g["c3_expected"])
+    ch = MbufChains.contiguous(arena, g["c5_off"], 9000)
+    got = u.in_cksum_pseudo_header_batch(ch.heads, 8980, 20, g["c5_src"], g["c5_dst"], g["c5_proto"])
+    np.testing.assert_array_equal(got, g["c5_expected"])
+
+
+def test_pcap_kat_gpu(torch_dev, pcap_frames):
+    arena, off, ln, hl, plen, src, dst = pcap_cases(pcap_frames)
+    assert not u.in_cksum_hdr_batch(arena.ctypes.data + off.astype(np.uint64)).any()
+    ch = MbufChains.contiguous(arena, off, ln)
+    assert not u.in_cksum_pseudo_header_batch(ch.heads, plen, hl, src, dst, 6).any()
+
+
+def test_host_batch_threads(torch_dev, ora):
+    """Concurrent callers (RX threads + TX app threads)."""
+    rng = np.random.default_rng(77)
+    arena = rand_arena(1 << 20, 77)
+    seg_off, seg_len, pkt_seg = random_chain_layout(rng, 4000, arena.size)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1])
+    want = ora.skip_batch(ch.heads, tot, 0)
+    results, errors = {}, []
+
+    def worker(k):
+        try:
+            sl = slice(k * 1000, (k + 1) * 1000)
+            for _ in range(5):
+                results[k] = u.in_cksum_skip_batch(ch.heads[sl], tot[sl], 0)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+    np.testing.assert_array_equal(np.concatenate([results[k] for k in range(4)]), want)
+
+
+# ---- BASELINE.json sizes --------------------------------------------------------
+
+def test_full_config2(torch_dev, ora):
+    """1 M x 1500 B contiguous packets (config 2), stride 1500 and the RX
+    stride-1514/+14 variant, whole batch vs the oracle."""
+    torch = torch_dev
+    n = 1 << 20
+    for stride, base in ((1500, 0), (1514, 14)):
+        d = torch.randint(0, 256, (base + stride * n + 64,), dtype=torch.uint8, device="cuda")
+        off = base + stride * torch.arange(n, dtype=torch.int64, device="cuda")
+        ln = torch.full((n,), 1500, dtype=torch.int32, device="cuda")
+        got = u.cksum_spans(d, off, ln, len_hint=1500)
+        got_s = u.cksum_strided(d[base:], stride, 1500, n)
+        want = ora.spans(d.cpu().numpy(), off.cpu().numpy(), 1500)
+        np.testing.assert_array_equal(host16(got), want)
+        np.testing.assert_array_equal(host16(got_s), want)
+        del d
+
+
+def test_full_config3_chains(torch_dev, ora):
+    """1 M mixed 64/576/1500-B packets as m_fragment-style chains of 1..256-B
+    segments at random 0-7-B offsets, skip 20 (config 3)."""
+    from libuinet_amd.workloads import config3_device
+
+    c = config3_device(1 << 20, seed=3)
+    got = u.cksum_chains(c["arena"], c["seg_off"], c["seg_len"], c["pkt_seg"], length=c["len"],
+                         skip=c["skip"], len_hint=c["mean_seg"])
+    lay = c["layout"]
+    want = ora.chains(c["arena"].cpu().numpy(), lay["seg_off"], lay["seg_len"], lay["pkt_seg"],
+                      length=lay["lens"], skip=20)
+    np.testing.assert_array_equal(host16(got), want)
+
+
+def test_config3_host_layout_matches_device(torch_dev):
+    """The host and device config-3 builders place identical bytes."""
+    from libuinet_amd.workloads import build_config3, config3_device
+
+    h = build_config3(4096, seed=9)
+    d = config3_device(4096, seed=9)
+    np.testing.assert_array_equal(d["arena"].cpu().numpy(), h["arena"])
+
+
+@pytest.mark.parametrize("hint", HINTS)
+def test_chains_len_skip(torch_dev, ora, hint):
+    """in_cksum_skip(chain, len, skip) semantics on device chains: skip
+    landing inside / exactly on segment boundaries, len short of, equal to
+    and beyond the chain, len <= skip."""
+    torch = torch_dev
+    rng = np.random.default_rng(4000 + hint)
+    arena = rand_arena(1 << 20, 41)
+    seg_off, seg_len, pkt_seg = random_chain_layout(rng, 4000, arena.size)
+    n = pkt_seg.size - 1
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1])
+    cum = np.concatenate([[0], np.cumsum(seg_len)])
+    skip = (rng.random(n) * (tot + 1)).astype(np.int64)
+    k = pkt_seg[:-1] + (rng.random(n) * np.diff(pkt_seg)).astype(np.int64)
+    skip = np.where(rng.random(n) < 0.25, cum[k] - cum[pkt_seg[:-1]], skip)
+    length = skip + (rng.random(n) * (tot - skip + 40)).astype(np.int64)
+    length = np.where(rng.random(n) < 0.1, skip - rng.integers(0, 3, n), length)
+    length = np.maximum(length, 0)
+    want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    np.testing.assert_array_equal(want, ora.skip_batch(ch.heads, length, skip))
+    got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
+                         dev(torch, pkt_seg.astype(np.int32)),
+                         length=dev(torch, length.astype(np.int32)),
+                         skip=dev(torch, skip.astype(np.int32)), len_hint=hint)
+    np.testing.assert_array_equal(host16(got), want)
+
+
+def test_full_config5_jumbo(torch_dev, ora):
+    """131072 x 9000-B jumbo frames, in_cksum_pseudo_header(m, 8980, 20, ...)
+    semantics via seeds (config 5); the host batch API on a slice."""
+    torch = torch_dev
+    n = 131072
+    rng = np.random.default_rng(55)
+    d = torch.randint(0, 256, (9000 * n,), dtype=torch.uint8, device="cuda")
+    host = d.cpu().numpy()
+    src = rng.integers(0, 2**32, n, dtype=np.uint64)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64)
+    proto = rng.choice([6, 17], n).astype(np.uint64)
+    bs = lambda x: ((x & 0xFF) << 8) | (x >> 8)  # noqa: E731
+    seed64 = src + dst + bs(proto) + bs(np.uint64(8980))
+    seed = ((seed64 & 0xFFFFFFFF) + (seed64 >> 32)).astype(np.uint64)
+    seed = ((seed & 0xFFFF) + (seed >> 16)).astype(np.uint32)
+    off = 9000 * np.arange(n, dtype=np.int64) + 20
+    got = u.cksum_spans(d, dev(torch, off), dev(torch, np.full(n, 8980, np.int32)),
+                        seed=dev(torch, seed.view(np.int32)), len_hint=8980)
+    want = ora.spans(host, off, 8980, seed)
+    np.testing.assert_array_equal(host16(got), want)
+    # cross-check the seed convention against the per-packet pseudo-header walk
+    ch = MbufChains.contiguous(host, 9000 * np.arange(256, dtype=np.int64), 9000)
+    np.testing.assert_array_equal(
+        ora.pseudo_header_batch(ch.heads, 8980, 20, src[:256], dst[:256], proto[:256]), want[:256])
+    np.testing.assert_array_equal(
+        u.in_cksum_pseudo_header_batch(ch.heads, 8980, 20, src[:256], dst[:256], proto[:256]),
+        want[:256])

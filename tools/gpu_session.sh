@@ -1,0 +1,34 @@
+#!/usr/bin/env bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel trace + PMC pass.
+# Each GPU step has its own time limit; a fault/abort/timeout ends the script.
+# Usage: tools/gpu_session.sh <tag> [tests|bench|prof|all]
+set -u
+TAG=${1:-r01}
+WHAT=${2:-all}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+fatal() { # exit codes that mean the GPU step crashed or hung
+  case "$1" in 124|134|137|139) return 0;; *) return 1;; esac
+}
+run() { # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -n 5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL step $name rc=$rc -- stopping"; exit $rc; fi
+  return 0
+}
+if [[ $WHAT == all || $WHAT == tests ]]; then
+  run pytest_gpu 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+fi
+if [[ $WHAT == all || $WHAT == bench ]]; then
+  run bench 600 python bench.py --steps 50 --warmup 10
+  run bench_strided 300 python bench.py --steps 50 --warmup 10 --api strided --cpu-baseline off
+fi
+if [[ $WHAT == all || $WHAT == prof ]]; then
+  run prof_trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline off
+  run prof_pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats -d "$OUT/prof_pmc" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline off
+fi
+echo "== done"
