@@ -6,10 +6,10 @@
 // complemented (in_cksum_skip :193-232, in_cksum_pseudo_header :241-276,
 // in_cksum_hdr :278-285).  The kernels reproduce it bit for bit:
 //
-//  * Loads are 16-byte aligned `global_load_dwordx4`s of the chunks that
-//    hold at least one byte of a span (an aligned 16-B chunk never crosses a
-//    page, so the over-read at a span's head and tail can never fault --
-//    the same property in_cksumdata relies on, in_cksum.c:106-115,165-167).
+//  * Loads are 16-byte aligned, non-temporal `global_load_dwordx4`s of the
+//    chunks that hold at least one byte of a span (an aligned 16-B chunk
+//    never crosses a page, so the over-read at a span's head and tail cannot
+//    fault -- the property in_cksumdata relies on, in_cksum.c:106-115,165-167).
 //    Bytes outside the span are masked off in registers.
 //  * Each lane sums the 32-bit words of its chunks in a 64-bit register.  A
 //    word loaded from an aligned address weights its bytes by 256^(addr&1)
@@ -19,11 +19,16 @@
 //  * Folding is always end-around carry, never "% 65535", so an all-zero
 //    packet (sum 0 -> 0xffff) stays distinct from a sum of 0xffff (-> 0).
 //  * G lanes own one packet (G = 8..64 picked from the mean length); a
-//    packet's lanes issue U loads back to back before summing, and the G
-//    partial sums meet in a butterfly of cross-lane shuffles.  No LDS and no
-//    MFMA: this is an HBM-bound integer fold (~0.25 adds per byte).
+//    packet's lanes issue U loads back to back, the next packet's
+//    descriptors are fetched behind them, and the G partial sums meet in a
+//    butterfly of cross-lane shuffles.  No LDS and no MFMA: an HBM-bound
+//    integer fold (~0.25 adds per byte).
+//
+// Index arithmetic is 32-bit (a span is < 2 GiB) and addresses are formed by
+// pointer arithmetic only, so every load stays in the global address space.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "cksum_internal.h"
 
@@ -31,6 +36,8 @@ namespace uinet {
 namespace {
 
 constexpr int kBlock = 256;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t fold16(uint64_t s) {
   uint64_t t = (s & 0xffffffffull) + (s >> 32);  // <= 2^33
@@ -44,59 +51,88 @@ __device__ __forceinline__ uint32_t rot8(uint32_t x) {  // x * 256 mod 65535
   return ((x << 8) | (x >> 8)) & 0xffff;
 }
 
-// Mask of bytes [s, e) of a 64-bit little-endian half-chunk; s, e may lie
-// outside [0, 8] and are clamped.
+__device__ __forceinline__ int clampi(int x, int lo, int hi) { return min(max(x, lo), hi); }
+
+// Mask of bytes [s, e) of an 8-byte little-endian half-chunk (s, e clamped).
 __device__ __forceinline__ uint64_t byte_mask64(int s, int e) {
-  s = min(max(s, 0), 8);
-  e = min(max(e, 0), 8);
+  s = clampi(s, 0, 8);
+  e = clampi(e, 0, 8);
   const uint64_t lo = (s >= 8) ? 0ull : (~0ull << (8 * s));
   const uint64_t hi = (e >= 8) ? ~0ull : ~(~0ull << (8 * e));
   return lo & hi;
 }
 
 // Sum of the 32-bit words of one 16-byte chunk restricted to bytes [s, e).
-__device__ __forceinline__ uint64_t chunk_sum(uint4 v, int s, int e) {
-  uint64_t a = ((uint64_t)v.y << 32) | v.x;
-  uint64_t b = ((uint64_t)v.w << 32) | v.z;
-  a &= byte_mask64(s, e);
-  b &= byte_mask64(s - 8, e - 8);
-  return (a & 0xffffffffull) + (a >> 32) + (b & 0xffffffffull) + (b >> 32);
+__device__ __forceinline__ uint64_t chunk_sum(u32x4 v, int s, int e) {
+  s = clampi(s, 0, 16);
+  e = clampi(e, 0, 16);
+  const uint64_t m0 = byte_mask64(s, e);
+  const uint64_t m1 = byte_mask64(s - 8, e - 8);
+  const uint32_t w0 = v.x & (uint32_t)m0;
+  const uint32_t w1 = v.y & (uint32_t)(m0 >> 32);
+  const uint32_t w2 = v.z & (uint32_t)m1;
+  const uint32_t w3 = v.w & (uint32_t)(m1 >> 32);
+  return (uint64_t)w0 + w1 + w2 + w3;
 }
 
-__device__ __forceinline__ uint4 load16(const uint8_t* p) {
-  return *reinterpret_cast<const uint4*>(p);
+__device__ __forceinline__ u32x4 load_chunk(const uint8_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
 
-// Per-lane partial sum of the span [a, a + len) over the G lanes of a group.
-// Chunk k (relative to the aligned-down start) goes to lane k mod G; lanes
-// past the last chunk re-load the last chunk (same cache line, so the load
-// coalesces with a live lane's) and mask it away completely.
+// One span [a, a + len) seen by the G lanes of a group, in rounds of G*U
+// chunks; chunk k (relative to the 16-B aligned-down start c0) belongs to
+// lane k mod G.  Lanes past the last chunk re-load the last chunk (the same
+// cache line as a live lane's load) and mask it away completely.
 template <int G, int U>
-__device__ __forceinline__ uint64_t span_lane_sum(const uint8_t* a, uint32_t len, int gl) {
-  const uintptr_t ua = reinterpret_cast<uintptr_t>(a);
-  const uint8_t* c0 = reinterpret_cast<const uint8_t*>(ua & ~uintptr_t(15));
-  const int head = (int)(ua & 15);
-  const uint32_t nch = (uint32_t)((head + (uint64_t)len + 15) >> 4);
-  uint64_t acc = 0;
-  if (nch == 0) return 0;
-  for (uint32_t k0 = 0; k0 < nch; k0 += G * U) {
-    uint4 v[U];
+struct Span {
+  const uint8_t* c0;
+  int head;      // a - c0, 0..15
+  int end;       // head + len
+  uint32_t nch;  // chunks holding at least one byte
+  u32x4 v[U];
+
+  __device__ __forceinline__ void init(const uint8_t* a, uint32_t len) {
+    head = (int)(reinterpret_cast<uintptr_t>(a) & 15);
+    c0 = a - head;
+    end = head + (int)len;
+    nch = (uint32_t)(end + 15) >> 4;
+  }
+  __device__ __forceinline__ void load(uint32_t k0, int gl) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t k = min(k0 + (uint32_t)(u * G + gl), nch - 1);
-      v[u] = load16(c0 + 16ull * k);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t k = (int64_t)k0 + u * G + gl;
-      const int64_t s = (int64_t)head - 16 * k;
-      const int64_t e = s + (int64_t)len;
-      // Interior chunks (the common case) have s <= 0 and e >= 16; the
-      // clamps below turn everything else into exact byte masks.
-      acc += chunk_sum(v[u], (int)max<int64_t>(min<int64_t>(s, 16), -16),
-                       (int)max<int64_t>(min<int64_t>(e, 32), -16));
+      v[u] = load_chunk(c0 + 16u * k);
     }
   }
+  __device__ __forceinline__ uint64_t sum(uint32_t k0, int gl) const {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = 16 * (int)(k0 + (uint32_t)(u * G + gl));
+      acc += chunk_sum(v[u], head - b, end - b);
+    }
+    return acc;
+  }
+  // The rounds after the first (spans longer than G*U chunks).
+  __device__ __forceinline__ uint64_t rest(int gl) {
+    uint64_t acc = 0;
+    for (uint32_t k0 = G * U; k0 < nch; k0 += G * U) {
+      load(k0, gl);
+      acc += sum(k0, gl);
+    }
+    return acc;
+  }
+};
+
+// Whole-span lane sum (no prefetch interleave): used by the chain walker.
+template <int G, int U>
+__device__ __forceinline__ uint64_t span_lane_sum(const uint8_t* a, uint32_t len, int gl) {
+  if (len == 0) return 0;
+  Span<G, U> sp;
+  sp.init(a, len);
+  sp.load(0, gl);
+  uint64_t acc = sp.sum(0, gl);
+  if (sp.nch > (uint32_t)(G * U)) acc += sp.rest(gl);
   return acc;
 }
 
@@ -116,44 +152,49 @@ __device__ __forceinline__ uint16_t finish(uint64_t s, uint32_t flags) {
 }
 
 // ---- one span per packet -------------------------------------------------
+//
+// Software-pipelined over the packets a group owns (p, p + stride, ...): the
+// data loads of packet p are issued first, then the descriptors of the next
+// packet, so waiting for p's bytes never waits for the prefetch and the
+// prefetch latency hides under p's fold.
 
-template <int G, int U>
+template <int G, int U, bool kStrided>
 __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ base,
                                                  const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ len,
                                                  const uint32_t* __restrict__ seed,
                                                  const uint8_t* __restrict__ parity,
+                                                 uint64_t pkt_stride, uint32_t fixed_len,
                                                  uint16_t* __restrict__ out, uint32_t n,
                                                  uint32_t flags) {
   constexpr uint32_t kGroups = kBlock / G;
   const int gl = threadIdx.x & (G - 1);
   const uint32_t stride = gridDim.x * kGroups;
-  for (uint32_t p = blockIdx.x * kGroups + threadIdx.x / G; p < n; p += stride) {
-    const uint8_t* a = base + off[p];
-    const uint64_t acc = span_lane_sum<G, U>(a, len[p], gl);
+  uint32_t p = blockIdx.x * kGroups + threadIdx.x / G;
+  if (p >= n) return;  // whole groups leave together
+  uint64_t o = kStrided ? (uint64_t)p * pkt_stride : off[p];
+  uint32_t l = kStrided ? fixed_len : len[p];
+  for (;;) {
+    const uint8_t* a = base + o;
+    Span<G, U> sp;
+    sp.init(a, l);
+    if (l) sp.load(0, gl);
+    // prefetch the next packet's descriptors behind this packet's loads
+    const uint32_t pn = p + stride;
+    const uint32_t pc = min(pn, n - 1);
+    const uint64_t on = kStrided ? (uint64_t)pc * pkt_stride : off[pc];
+    const uint32_t ln = kStrided ? fixed_len : len[pc];
+    uint64_t acc = l ? sp.sum(0, gl) : 0;
+    if (sp.nch > (uint32_t)(G * U)) acc += sp.rest(gl);
     uint32_t x = fold16(acc);
     const uint32_t lp = parity ? parity[p] : 0u;
     if ((lp ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
     x = group_sum<G>(x);
     if (gl == 0) out[p] = finish((uint64_t)x + (seed ? seed[p] : 0u), flags);
-  }
-}
-
-template <int G, int U>
-__global__ __launch_bounds__(kBlock) void k_strided(const uint8_t* __restrict__ base,
-                                                   uint64_t pkt_stride, uint32_t len,
-                                                   const uint32_t* __restrict__ seed,
-                                                   uint16_t* __restrict__ out, uint32_t n,
-                                                   uint32_t flags) {
-  constexpr uint32_t kGroups = kBlock / G;
-  const int gl = threadIdx.x & (G - 1);
-  const uint32_t stride = gridDim.x * kGroups;
-  for (uint32_t p = blockIdx.x * kGroups + threadIdx.x / G; p < n; p += stride) {
-    const uint8_t* a = base + (uint64_t)p * pkt_stride;
-    uint32_t x = fold16(span_lane_sum<G, U>(a, len, gl));
-    if (reinterpret_cast<uintptr_t>(a) & 1) x = rot8(x);
-    x = group_sum<G>(x);
-    if (gl == 0) out[p] = finish((uint64_t)x + (seed ? seed[p] : 0u), flags);
+    if (pn >= n) break;
+    p = pn;
+    o = on;
+    l = ln;
   }
 }
 
@@ -181,18 +222,18 @@ __global__ __launch_bounds__(kBlock) void k_chains(const uint8_t* __restrict__ b
   const uint32_t stride = gridDim.x * kGroups;
   for (uint32_t p = blockIdx.x * kGroups + threadIdx.x / G; p < n; p += stride) {
     const uint32_t s0 = pkt_seg[p], s1 = pkt_seg[p + 1];
-    const uint64_t lo_want = pskip ? pskip[p] : 0u;
-    const uint64_t hi_want = plen ? (uint64_t)plen[p] : ~0ull;
+    const uint32_t lo_want = pskip ? pskip[p] : 0u;
+    const uint32_t hi_want = plen ? plen[p] : 0xffffffffu;
     uint64_t tot = 0;
-    uint64_t pos = 0;  // chain offset of segment s
+    uint32_t pos = 0;  // chain offset of segment s
     for (uint32_t s = s0; s < s1 && pos < hi_want; ++s) {
-      const uint64_t l = seg_len[s];
-      const uint64_t lo = lo_want > pos ? min(lo_want - pos, l) : 0;
-      const uint64_t hi = min(hi_want - pos, l);
+      const uint32_t l = seg_len[s];
+      const uint32_t lo = lo_want > pos ? min(lo_want - pos, l) : 0u;
+      const uint32_t hi = min(hi_want - pos, l);
       if (hi > lo) {
         const uint8_t* a = base + seg_off[s] + lo;
-        uint32_t x = fold16(span_lane_sum<G, U>(a, (uint32_t)(hi - lo), gl));
-        const uint32_t lpar = (uint32_t)(pos + lo - lo_want);  // logical offset
+        uint32_t x = fold16(span_lane_sum<G, U>(a, hi - lo, gl));
+        const uint32_t lpar = pos + lo - lo_want;  // logical offset of a
         if ((lpar ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
         tot += x;
       }
@@ -209,8 +250,8 @@ struct Geometry {
   int g, u;
 };
 
-// Lanes per packet and loads in flight per lane from the mean packet length:
-// aim for one unrolled round per packet with most lanes holding a chunk.
+// Lanes per packet and loads in flight per lane from the mean length: one
+// unrolled round per packet with most lanes holding a chunk.
 Geometry pick_geometry(uint32_t mean_len) {
   if (mean_len == 0) return {64, 2};
   if (mean_len <= 96) return {8, 1};
@@ -220,11 +261,24 @@ Geometry pick_geometry(uint32_t mean_len) {
   return {64, 3};
 }
 
-int grid_for(uint32_t n, int g) {
+// Blocks per CU of the grid-stride launch.  Measured on MI355X (config 2,
+// profiles/r01): the span kernel peaks at 64 (8 packets per group -- enough
+// rounds for the descriptor prefetch to pay, few enough that the tail is
+// short); the strided kernel has no descriptors and prefers one packet per
+// group (no cap).  UINET_CKSUM_BLOCKS_PER_CU overrides both.
+int blocks_per_cu(int dflt) {
+  static int v = [] {
+    const char* e = getenv("UINET_CKSUM_BLOCKS_PER_CU");
+    const int x = e ? atoi(e) : 0;
+    return (x > 0 && x <= 4096) ? x : 0;
+  }();
+  return v ? v : dflt;
+}
+
+int grid_for(uint32_t n, int g, int bpc = 64) {
   const uint32_t groups_per_block = kBlock / g;
   uint64_t blocks = ((uint64_t)n + groups_per_block - 1) / groups_per_block;
-  // Enough blocks to fill 256 CUs at full occupancy, then grid-stride.
-  const uint64_t cap = 256ull * 8;
+  const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(bpc);
   if (blocks > cap) blocks = cap;
   if (blocks == 0) blocks = 1;
   return (int)blocks;
@@ -248,9 +302,10 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = pick_geometry(len_hint);
   const int grid = grid_for(n, geo.g);
-#define L(G, U)                                                                   \
-  hipLaunchKernelGGL((k_spans<G, U>), dim3(grid), dim3(kBlock), 0, stream,        \
-                     static_cast<const uint8_t*>(base), off, len, seed, parity, out, n, flags)
+#define L(G, U)                                                                    \
+  hipLaunchKernelGGL((k_spans<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,  \
+                     static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, out, \
+                     n, flags)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
@@ -260,10 +315,11 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
                    uint16_t* out, uint32_t n, uint32_t flags, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = pick_geometry(len);
-  const int grid = grid_for(n, geo.g);
-#define L(G, U)                                                                  \
-  hipLaunchKernelGGL((k_strided<G, U>), dim3(grid), dim3(kBlock), 0, stream,     \
-                     static_cast<const uint8_t*>(base), pkt_stride, len, seed, out, n, flags)
+  const int grid = grid_for(n, geo.g, 4096);
+#define L(G, U)                                                                     \
+  hipLaunchKernelGGL((k_spans<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,    \
+                     static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
+                     pkt_stride, len, out, n, flags)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();

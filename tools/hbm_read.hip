@@ -1,0 +1,99 @@
+// Read-bandwidth microbenchmark for MI355X (measurement tool, not product):
+// what a pure streaming read of a >= 1.5 GB buffer achieves with 16-byte
+// loads, by grid size, loads in flight per lane and cache policy.  Sets the
+// "achievable" ceiling the checksum kernel is compared against.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+  fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_read(const uint4* __restrict__ p, uint64_t n16,
+                                              uint32_t* __restrict__ sink) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  uint64_t i = tid;
+  for (; i + (U - 1) * nthr < n16; i += U * nthr) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + i + u * nthr));
+        v[u] = make_uint4(t.x, t.y, t.z, t.w);
+      } else {
+        v[u] = p[i + u * nthr];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+  }
+  for (; i < n16; i += nthr) { uint4 v = p[i]; acc += v.x + v.y + v.z + v.w; }
+  if (acc == 0x12345678u) sink[0] = acc;  // keep the loads live
+}
+
+// Contiguous-chunk variant: each block streams its own contiguous slice
+// (locality per CU) instead of a grid-wide stride.
+template <int U>
+__global__ __launch_bounds__(256) void k_read_chunk(const uint4* __restrict__ p, uint64_t n16,
+                                                    uint32_t* __restrict__ sink) {
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = blockIdx.x * per, b1 = min(n16, b0 + per);
+  uint32_t acc = 0;
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += U * 256) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t j = min(i + u * 256, b1 - 1);
+      v[u] = p[j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <typename F>
+float time_it(F f, int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  f(); f();
+  CK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(a)); f(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b)); if (ms < best) best = ms;
+  }
+  return best;
+}
+
+int main(int argc, char** argv) {
+  const uint64_t bytes = (argc > 1 ? strtoull(argv[1], 0, 0) : (1572864000ull));
+  const uint64_t n16 = bytes / 16;
+  uint4* p; uint32_t* sink;
+  CK(hipMalloc(&p, bytes)); CK(hipMalloc(&sink, 64));
+  CK(hipMemset(p, 0x5a, bytes));
+  printf("{\"bytes\": %llu, \"results\": [\n", (unsigned long long)bytes);
+  bool first = true;
+  auto report = [&](const char* name, int grid, float ms) {
+    printf("%s {\"kernel\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", first ? "" : ",",
+           name, grid, ms, bytes / (ms * 1e-3) / 1e9);
+    first = false;
+  };
+  const int grids[] = {1024, 2048, 4096, 8192, 16384, 65536};
+  for (int g : grids) {
+    report("stride_u1", g, time_it([&] { k_read<1, false><<<g, 256>>>(p, n16, sink); }, 20));
+    report("stride_u2", g, time_it([&] { k_read<2, false><<<g, 256>>>(p, n16, sink); }, 20));
+    report("stride_u4", g, time_it([&] { k_read<4, false><<<g, 256>>>(p, n16, sink); }, 20));
+    report("stride_u8", g, time_it([&] { k_read<8, false><<<g, 256>>>(p, n16, sink); }, 20));
+    report("stride_u4_nt", g, time_it([&] { k_read<4, true><<<g, 256>>>(p, n16, sink); }, 20));
+    report("chunk_u4", g, time_it([&] { k_read_chunk<4><<<g, 256>>>(p, n16, sink); }, 20));
+    report("chunk_u8", g, time_it([&] { k_read_chunk<8><<<g, 256>>>(p, n16, sink); }, 20));
+  }
+  printf("]}\n");
+  return 0;
+}
