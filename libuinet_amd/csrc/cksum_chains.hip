@@ -1,0 +1,261 @@
+// MI355X (gfx950) chain kernels: in_cksum_skip(m, len, skip) over
+// device-resident mbuf chains given as segment lists.
+//
+// Packet p is the chain of segments [pkt_seg[p], pkt_seg[p+1]) (one segment
+// per mbuf, in m_next order); the chain bytes [skip, len) are summed exactly
+// as the reference walk does (/root/reference/sys/amd64/amd64/in_cksum.c
+// :203-229 -- len counts from the chain start, zero-length mbufs contribute
+// nothing, a short chain sums what it has), with the logical parity counted
+// from `skip`.  len == NULL means "the whole chain", skip == NULL means 0.
+//
+// k_chains_flat (default) -- a wave owns a tile of 32 consecutive packets and
+// therefore a contiguous range of segments, processed in descriptor rounds of
+// 64 segments (one per lane):
+//   * per segment: its packet slot (LDS start markers + a DPP max-scan), its
+//     chain position (a DPP segmented scan of the lengths keyed by slot,
+//     carried across rounds), the clip to [skip, len), its chunk count;
+//   * the round's segments become one concatenated list of 16-byte chunks
+//     (DPP scan of the chunk counts) that the wave sweeps 64 chunks per pass,
+//     kPass passes in flight -- every load is a dense 1 KiB whatever the
+//     segment lengths;
+//   * a chunk finds its segment by LDS start markers + a DPP max-scan, its
+//     bytes are masked with one ds_read_b128 from a 17x17 mask table, its
+//     fold is byte-rotated on its own (rotation is linear mod 65535);
+//   * chunk sums are binned per packet with a plain DPP prefix sum P: the
+//     last lane of each run of equal slots adds +P to its slot and -P to the
+//     next run's slot (telescoping), into the wave's u64 LDS accumulators.
+// k_chains (UINET_CKSUM_CHAINS=serial, kept for A/B) -- G lanes walk one
+// packet's segments one after another.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "cksum_device.h"
+
+namespace uinet {
+namespace {
+
+template <int G, int U>
+__global__ __launch_bounds__(kBlock) void k_chains(const uint8_t* __restrict__ base,
+                                                  const uint64_t* __restrict__ seg_off,
+                                                  const uint32_t* __restrict__ seg_len,
+                                                  const uint32_t* __restrict__ pkt_seg,
+                                                  const uint32_t* __restrict__ plen,
+                                                  const uint32_t* __restrict__ pskip,
+                                                  const uint32_t* __restrict__ seed,
+                                                  uint16_t* __restrict__ out, uint32_t n,
+                                                  uint32_t flags) {
+  constexpr uint32_t kGroups = kBlock / G;
+  const int gl = threadIdx.x & (G - 1);
+  const uint32_t stride = gridDim.x * kGroups;
+  for (uint32_t p = blockIdx.x * kGroups + threadIdx.x / G; p < n; p += stride) {
+    const uint32_t s0 = pkt_seg[p], s1 = pkt_seg[p + 1];
+    const uint32_t lo_want = pskip ? pskip[p] : 0u;
+    const uint32_t hi_want = plen ? plen[p] : 0xffffffffu;
+    uint64_t tot = 0;
+    uint32_t pos = 0;  // chain offset of segment s
+    for (uint32_t s = s0; s < s1 && pos < hi_want; ++s) {
+      const uint32_t l = seg_len[s];
+      const uint32_t lo = lo_want > pos ? min(lo_want - pos, l) : 0u;
+      const uint32_t hi = min(hi_want - pos, l);
+      if (hi > lo) {
+        const uint8_t* a = base + seg_off[s] + lo;
+        uint32_t x = fold16(span_lane_sum<G, U>(a, hi - lo, gl));
+        const uint32_t lpar = pos + lo - lo_want;  // logical offset of a
+        if ((lpar ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
+        tot += x;
+      }
+      pos += l;
+    }
+    const uint32_t x = group_sum<G>(fold16(tot));
+    if (gl == 0) out[p] = finish((uint64_t)x + (seed ? seed[p] : 0u), flags);
+  }
+}
+
+constexpr int kTile = 32;              // packets per wave tile
+constexpr int kWaves = kBlock / 64;
+
+template <int kPass>
+__global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restrict__ base,
+                                                       const uint64_t* __restrict__ seg_off,
+                                                       const uint32_t* __restrict__ seg_len,
+                                                       const uint32_t* __restrict__ pkt_seg,
+                                                       const uint32_t* __restrict__ plen,
+                                                       const uint32_t* __restrict__ pskip,
+                                                       const uint32_t* __restrict__ seed,
+                                                       uint16_t* __restrict__ out, uint32_t n,
+                                                       uint32_t flags) {
+  constexpr int kWin = 64 * kPass;  // chunks per batch of passes
+  __shared__ MaskLut lut;
+  __shared__ unsigned long long lds_acc[kWaves][kTile];
+  __shared__ uint32_t lds_pkmark[kWaves][64];   // packet-start markers (slot + 1)
+  __shared__ uint8_t lds_mark[kWaves][kWin];     // segment-start markers (lane + 1)
+  lut.init();
+  for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kWaves * kWin; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  unsigned long long* acc = lds_acc[wid];
+  uint32_t* pkmark = lds_pkmark[wid];
+  uint8_t* mark = lds_mark[wid];
+  const uint32_t tiles = (n + kTile - 1) / kTile;
+  const uint32_t wstride = gridDim.x * kWaves;
+  for (uint32_t t = blockIdx.x * kWaves + wid; t < tiles; t += wstride) {
+    const uint32_t P0 = t * kTile;
+    const int np = (int)min((uint32_t)kTile, n - P0);
+    const uint32_t ps = pkt_seg[P0 + (uint32_t)min(lane, np)];
+    const uint32_t k_skip = (lane < np && pskip) ? pskip[P0 + lane] : 0u;
+    const uint32_t k_len = (lane < np) ? (plen ? plen[P0 + lane] : 0xffffffffu) : 0u;
+    const uint32_t S0 = __builtin_amdgcn_readfirstlane(ps);
+    const uint32_t S1 = __builtin_amdgcn_readlane(ps, np);
+    if (lane < kTile) acc[lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    uint32_t carry_slot1 = 0;  // slot + 1 of the last segment of the previous round
+    uint32_t carry_pos = 0;    // chain offset just past that segment
+    for (uint32_t r0 = S0; r0 < S1; r0 += 64) {
+      // --- descriptor round: one segment per lane -------------------------
+      const uint32_t s = r0 + (uint32_t)lane;
+      const bool live = s < S1;
+      const uint32_t sc = live ? s : S1 - 1;
+      const uint64_t so = seg_off[sc];
+      const uint32_t l = live ? seg_len[sc] : 0u;
+      // packet slot: packets starting inside this round mark their first
+      // segment; a max-scan carries the latest start to every segment
+      const bool pk_in = lane < np && ps >= r0 && ps < r0 + 64;
+      if (pk_in) atomicMax(&pkmark[ps - r0], (uint32_t)lane + 1);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const uint32_t slot1 = max(wave_scan<1, false>(pkmark[lane], 0u), carry_slot1);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (pk_in) pkmark[ps - r0] = 0;
+      const uint32_t slot = slot1 - 1;
+      // chain position: segmented scan of the lengths, carried across rounds
+      const uint32_t pos = wave_scan<0, true>(l, slot) - l + (slot1 == carry_slot1 ? carry_pos : 0u);
+      carry_slot1 = __builtin_amdgcn_readlane(slot1, 63);
+      carry_pos = __builtin_amdgcn_readlane(pos + l, 63);
+      const uint32_t sk = __shfl(k_skip, (int)slot);
+      const uint32_t ln = __shfl(k_len, (int)slot);
+      const uint32_t lo = sk > pos ? min(sk - pos, l) : 0u;
+      const uint32_t hi = ln > pos ? min(ln - pos, l) : 0u;
+      const uint32_t eff = hi > lo ? hi - lo : 0u;
+      const uint64_t ao = so + lo;
+      const uint32_t head = eff ? (uint32_t)(reinterpret_cast<uintptr_t>(base + ao) & 15) : 0u;
+      const uint32_t nch = eff ? (head + eff + 15) >> 4 : 0u;
+      const uint64_t c0 = ao - head;  // offset of the segment's first chunk
+      const uint32_t rot = ((pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(base + ao)) & 1u;
+      const uint32_t meta = (slot << 1) | rot;
+      const uint32_t span = (eff << 4) | head;  // eff < 2^28
+      const uint32_t ci = wave_scan<0, false>(nch, 0u);
+      const uint32_t cst = ci - nch;  // first chunk of each segment in the round's list
+      const uint32_t C = __builtin_amdgcn_readlane(ci, 63);
+      const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
+      // --- data: batches of kPass passes over the round's chunk list ------
+      uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the pass
+      for (uint32_t b = 0; b < C; b += kWin) {
+        const bool mk = nch != 0 && cst >= b && cst < b + kWin;
+        if (mk) mark[cst - b] = (uint8_t)(lane + 1);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        u32x4 v[kPass];
+        int s_lo[kPass], s_hi[kPass];
+        uint32_t mt[kPass];
+#pragma unroll
+        for (int q = 0; q < kPass; ++q) {
+          const uint32_t c = b + (uint32_t)(q * 64 + lane);
+          const bool in = c < C;
+          const uint32_t seg1 = max(wave_scan<1, false>(mark[q * 64 + lane], 0u), carry_seg1);
+          carry_seg1 = __builtin_amdgcn_readlane(seg1, 63);
+          const int seg = (int)seg1 - 1;
+          // Cross-lane reads stay outside any condition: a ds_bpermute under
+          // a partial exec mask reads 0 from the inactive source lanes.
+          const uint32_t cst_seg = (uint32_t)__shfl(cst, seg);
+          const uint32_t k = in ? c - cst_seg : 0u;  // past the end: chunk 0, masked
+          const uint64_t cbase = ((uint64_t)(uint32_t)__shfl(c0_hi, seg) << 32) |
+                                 (uint32_t)__shfl(c0_lo, seg);
+          const uint32_t sp = __shfl(span, seg);
+          mt[q] = __shfl(meta, seg);
+          const int h = (int)(sp & 15), e = (int)(sp >> 4);
+          s_lo[q] = h - 16 * (int)k;
+          s_hi[q] = in ? h + e - 16 * (int)k : s_lo[q];
+          v[q] = load_chunk(base + cbase + 16ull * k);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (mk) mark[cst - b] = 0;
+#pragma unroll
+        for (int q = 0; q < kPass; ++q) {
+          uint32_t w = fold16(lut.sum(v[q], s_lo[q], s_hi[q]));
+          if (mt[q] & 1) w = rot8(w);
+          const uint32_t sl = mt[q] >> 1;
+          const uint32_t P = wave_scan<0, false>(w, 0u);
+          const uint32_t nx = __shfl_down(sl, 1);
+          if (lane == 63 || nx != sl) {
+            atomicAdd(&acc[sl], (unsigned long long)P);
+            if (lane != 63) atomicAdd(&acc[nx], (unsigned long long)(-(long long)P));
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane < np) {
+      const uint32_t p = P0 + (uint32_t)lane;
+      out[p] = finish(acc[lane] + (seed ? seed[p] : 0u), flags);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
+struct Geometry {
+  int g, u;
+};
+
+Geometry pick_serial(uint32_t mean_seg) {
+  if (mean_seg == 0) return {64, 2};
+  if (mean_seg <= 96) return {8, 1};
+  if (mean_seg <= 224) return {8, 2};
+  if (mean_seg <= 720) return {16, 3};
+  if (mean_seg <= 1520) return {32, 3};
+  return {64, 3};
+}
+
+}  // namespace
+
+int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
+                  const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
+                  const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                  uint32_t len_hint, hipStream_t stream) {
+  if (n == 0) return UINET_CKSUM_OK;
+  static const bool serial = [] {
+    const char* e = getenv("UINET_CKSUM_CHAINS");
+    return e && e[0] == 's';
+  }();
+  const uint8_t* b = static_cast<const uint8_t*>(base);
+  if (serial) {
+    // len_hint = mean SEGMENT length: the group walks one segment at a time
+    const Geometry geo = pick_serial(len_hint);
+    const uint32_t gpb = kBlock / geo.g;
+    uint64_t blocks = ((uint64_t)n + gpb - 1) / gpb;
+    const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
+    blocks = blocks > cap ? cap : blocks;
+#define L(G, U)                                                                              \
+  hipLaunchKernelGGL((k_chains<G, U>), dim3((int)blocks), dim3(kBlock), 0, stream, b, seg_off, \
+                     seg_len, pkt_seg, len, skip, seed, out, n, flags)
+    switch (geo.g * 16 + geo.u) {
+      case 8 * 16 + 1: L(8, 1); break;
+      case 8 * 16 + 2: L(8, 2); break;
+      case 16 * 16 + 3: L(16, 3); break;
+      case 32 * 16 + 3: L(32, 3); break;
+      case 64 * 16 + 2: L(64, 2); break;
+      default: L(64, 3); break;
+    }
+#undef L
+    return check_launch();
+  }
+  const uint32_t tiles = (n + kTile - 1) / kTile;
+  uint64_t blocks = (tiles + kWaves - 1) / kWaves;
+  const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
+  blocks = blocks > cap ? cap : blocks;
+  hipLaunchKernelGGL((k_chains_flat<4>), dim3((int)blocks), dim3(kBlock), 0, stream, b, seg_off,
+                     seg_len, pkt_seg, len, skip, seed, out, n, flags);
+  return check_launch();
+}
+
+}  // namespace uinet

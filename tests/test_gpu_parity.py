@@ -292,6 +292,35 @@ def test_config3_host_layout_matches_device(torch_dev):
     np.testing.assert_array_equal(d["arena"].cpu().numpy(), h["arena"])
 
 
+@pytest.mark.parametrize("hint", [0, 40, 200, 500])
+def test_chains_many_segments(torch_dev, ora, hint):
+    """Chains of 0..300 segments (the tiled kernel carries chain positions
+    across 64-segment descriptor rounds), empty chains, 1-byte segments."""
+    torch = torch_dev
+    rng = np.random.default_rng(7000 + hint)
+    arena = rand_arena(1 << 21, 43)
+    n = 700
+    nseg = rng.integers(0, 301, n)
+    nseg[rng.random(n) < 0.1] = 0
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = np.where(rng.random(s) < 0.3, rng.integers(0, 3, s), rng.integers(1, 80, s))
+    seg_off = rng.integers(0, arena.size - 100, s).astype(np.int64)
+    tot = np.zeros(n, np.int64)
+    nz = nseg > 0
+    tot[nz] = np.add.reduceat(seg_len, pkt_seg[:-1][nz])
+    skip = (rng.random(n) * (tot + 1) * 0.3).astype(np.int64)
+    length = skip + (rng.random(n) * (tot - skip + 10)).astype(np.int64)
+    seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
+    got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
+                         dev(torch, pkt_seg.astype(np.int32)),
+                         length=dev(torch, length.astype(np.int32)),
+                         skip=dev(torch, skip.astype(np.int32)),
+                         seed=dev(torch, seed.view(np.int32)), len_hint=hint)
+    np.testing.assert_array_equal(host16(got), want)
+
+
 @pytest.mark.parametrize("hint", HINTS)
 def test_chains_len_skip(torch_dev, ora, hint):
     """in_cksum_skip(chain, len, skip) semantics on device chains: skip
