@@ -192,14 +192,19 @@ def main():
     launch = make_launch(args.config, w, args.api, out)
     counts = [n] * world
     K, Wm = args.steps, args.warmup
+    # Kernel time from HIP events on the launch stream.  At N = 1 a step IS
+    # one launch, so one event pair brackets the K back-to-back launches (no
+    # per-launch event overhead; inter-launch gaps count against us).  At
+    # N > 1 each launch is bracketed so the gather stays out of it.
+    per_launch = world > 1
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)]
+          for _ in range(K if per_launch else 1)]
 
     def step(k=None):
-        if k is not None:
+        if per_launch and k is not None:
             ev[k][0].record(stream)
         launch(stream)
-        if k is not None:
+        if per_launch and k is not None:
             ev[k][1].record(stream)
         if world > 1:
             gather_results(out, counts)
@@ -211,8 +216,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if not per_launch:
+        ev[0][0].record(stream)
     for k in range(K):
         step(k)
+    if not per_launch:
+        ev[0][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -222,7 +231,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kms = np.array([a.elapsed_time(b) for a, b in ev])  # ms, kernel only
+    if per_launch:
+        kms = np.array([a.elapsed_time(b) for a, b in ev])  # ms, kernel only
+    else:
+        kms = np.array([ev[0][0].elapsed_time(ev[0][1]) / K])  # mean ms per launch
 
     result = None
     if rank == 0:

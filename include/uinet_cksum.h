@@ -105,6 +105,15 @@ int uinet_cksum_last_hip_error(void);
 /* 1 when a gfx950 device is visible to the calling thread, else 0. */
 int uinet_cksum_device_ok(void);
 
+/* Performance knobs (process-wide; they never change results):
+ *   "blocks_per_cu"   grid-stride launch width, 0 = per-kernel default
+ *   "chains_variant"  0 = flattened chunk stream (default), 1 = serial walk
+ *   "chains_pass"     passes in flight per wave in the chain kernel: 2, 4, 8
+ * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
+ * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
+ * (serial|flat) and UINET_CKSUM_CHAINS_PASS set the initial values. */
+int uinet_cksum_set_tuning(const char *key, int value);
+
 /* ------------------------------------------------------------------------ */
 /* 2b. Device-resident descriptor API (the hot path)                         */
 /*                                                                          */

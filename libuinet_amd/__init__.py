@@ -45,7 +45,7 @@ OK, EINVAL, ENODEV, ENOMEM, EHIP = 0, -22, -19, -12, -5
 EXPORTED_SYMBOLS = (
     "in_cksum_skip", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo", "in_addword",
     "uinet_cksum_version", "uinet_cksum_strerror", "uinet_cksum_last_hip_error",
-    "uinet_cksum_device_ok", "uinet_cksum_spans", "uinet_cksum_strided", "uinet_cksum_chains",
+    "uinet_cksum_device_ok", "uinet_cksum_set_tuning", "uinet_cksum_spans", "uinet_cksum_strided", "uinet_cksum_chains",
     "in_cksum_skip_batch", "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch",
 )
 
@@ -89,6 +89,7 @@ def lib() -> ctypes.CDLL:
         "uinet_cksum_strerror": (ctypes.c_char_p, [_i32]),
         "uinet_cksum_last_hip_error": (_i32, []),
         "uinet_cksum_device_ok": (_i32, []),
+        "uinet_cksum_set_tuning": (_i32, [ctypes.c_char_p, _i32]),
         "uinet_cksum_spans": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]),
         "uinet_cksum_strided": (_i32, [_vp, _u64, _u32, _vp, _vp, _u32, _u32, _vp]),
         "uinet_cksum_chains": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32,
@@ -269,6 +270,11 @@ def cksum_chains(base, seg_off, seg_len, pkt_seg, length=None, skip=None, seed=N
         _dp(base), _dp(seg_off), _dp(seg_len), _dp(pkt_seg), _dp(length), _dp(skip), _dp(seed),
         _dp(out), n, flags, len_hint, _stream(stream)))
     return out
+
+
+def set_tuning(key: str, value: int) -> None:
+    """uinet_cksum_set_tuning: performance knobs that never change results."""
+    _check("uinet_cksum_set_tuning", lib().uinet_cksum_set_tuning(key.encode(), value))
 
 
 def device_ok() -> bool:

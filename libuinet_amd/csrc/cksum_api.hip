@@ -53,6 +53,25 @@ int record_hip(hipError_t e) {
 
 int check_launch() { return record_hip(hipGetLastError()); }
 
+static Tuning& tuning_rw() {
+  static Tuning t = [] {
+    Tuning x{0, 0, 2};
+    if (const char* e = getenv("UINET_CKSUM_BLOCKS_PER_CU")) {
+      const int v = atoi(e);
+      x.blocks_per_cu = (v > 0 && v <= 4096) ? v : 0;
+    }
+    if (const char* e = getenv("UINET_CKSUM_CHAINS")) x.chains_variant = e[0] == 's' ? 1 : 0;
+    if (const char* e = getenv("UINET_CKSUM_CHAINS_PASS")) {
+      const int v = atoi(e);
+      if (v == 2 || v == 4 || v == 8) x.chains_pass = v;
+    }
+    return x;
+  }();
+  return t;
+}
+
+const Tuning& tuning() { return tuning_rw(); }
+
 namespace {
 
 uint32_t fold16_host(uint64_t s) {
@@ -305,6 +324,21 @@ const char* uinet_cksum_strerror(int code) {
 }
 
 int uinet_cksum_last_hip_error(void) { return t_last_hip; }
+
+int uinet_cksum_set_tuning(const char* key, int value) {
+  if (!key) return UINET_CKSUM_EINVAL;
+  Tuning& t = tuning_rw();
+  if (!strcmp(key, "blocks_per_cu") && value >= 0 && value <= 4096) {
+    t.blocks_per_cu = value;
+  } else if (!strcmp(key, "chains_variant") && (value == 0 || value == 1)) {
+    t.chains_variant = value;
+  } else if (!strcmp(key, "chains_pass") && (value == 2 || value == 4 || value == 8)) {
+    t.chains_pass = value;
+  } else {
+    return UINET_CKSUM_EINVAL;
+  }
+  return UINET_CKSUM_OK;
+}
 
 int uinet_cksum_device_ok(void) {
   int dev = 0, count = 0;

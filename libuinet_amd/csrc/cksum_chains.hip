@@ -113,13 +113,21 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     uint32_t carry_slot1 = 0;  // slot + 1 of the last segment of the previous round
     uint32_t carry_pos = 0;    // chain offset just past that segment
+    // descriptors one round ahead: round r+1's loads fly under round r's data
+    uint64_t so_next = 0;
+    uint32_t l_next = 0;
+    auto fetch = [&](uint32_t r) {
+      const uint32_t s = r + (uint32_t)lane;
+      const uint32_t sc = s < S1 ? s : S1 - 1;
+      so_next = seg_off[sc];
+      l_next = s < S1 ? seg_len[sc] : 0u;
+    };
+    if (S0 < S1) fetch(S0);
     for (uint32_t r0 = S0; r0 < S1; r0 += 64) {
       // --- descriptor round: one segment per lane -------------------------
-      const uint32_t s = r0 + (uint32_t)lane;
-      const bool live = s < S1;
-      const uint32_t sc = live ? s : S1 - 1;
-      const uint64_t so = seg_off[sc];
-      const uint32_t l = live ? seg_len[sc] : 0u;
+      const uint64_t so = so_next;
+      const uint32_t l = l_next;
+      if (r0 + 64 < S1) fetch(r0 + 64);
       // packet slot: packets starting inside this round mark their first
       // segment; a max-scan carries the latest start to every segment
       const bool pk_in = lane < np && ps >= r0 && ps < r0 + 64;
@@ -158,13 +166,24 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
         u32x4 v[kPass];
         int s_lo[kPass], s_hi[kPass];
         uint32_t mt[kPass];
+        // segment starts of all passes at once: independent max-scans, then
+        // the carries as a scalar prefix max (seg1 never decreases)
+        uint32_t sc1[kPass];
+#pragma unroll
+        for (int q = 0; q < kPass; ++q) sc1[q] = mark[q * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < kPass; ++q) sc1[q] = wave_scan<1, false>(sc1[q], 0u);
+#pragma unroll
+        for (int q = 0; q < kPass; ++q) {
+          const uint32_t last = __builtin_amdgcn_readlane(sc1[q], 63);
+          sc1[q] = max(sc1[q], carry_seg1);
+          carry_seg1 = max(carry_seg1, last);
+        }
 #pragma unroll
         for (int q = 0; q < kPass; ++q) {
           const uint32_t c = b + (uint32_t)(q * 64 + lane);
           const bool in = c < C;
-          const uint32_t seg1 = max(wave_scan<1, false>(mark[q * 64 + lane], 0u), carry_seg1);
-          carry_seg1 = __builtin_amdgcn_readlane(seg1, 63);
-          const int seg = (int)seg1 - 1;
+          const int seg = (int)sc1[q] - 1;
           // Cross-lane reads stay outside any condition: a ds_bpermute under
           // a partial exec mask reads 0 from the inactive source lanes.
           const uint32_t cst_seg = (uint32_t)__shfl(cst, seg);
@@ -223,12 +242,9 @@ int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg
                   const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
                   uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
-  static const bool serial = [] {
-    const char* e = getenv("UINET_CKSUM_CHAINS");
-    return e && e[0] == 's';
-  }();
+  const Tuning& tn = tuning();
   const uint8_t* b = static_cast<const uint8_t*>(base);
-  if (serial) {
+  if (tn.chains_variant == 1) {
     // len_hint = mean SEGMENT length: the group walks one segment at a time
     const Geometry geo = pick_serial(len_hint);
     const uint32_t gpb = kBlock / geo.g;
@@ -253,8 +269,16 @@ int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg
   uint64_t blocks = (tiles + kWaves - 1) / kWaves;
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
-  hipLaunchKernelGGL((k_chains_flat<4>), dim3((int)blocks), dim3(kBlock), 0, stream, b, seg_off,
-                     seg_len, pkt_seg, len, skip, seed, out, n, flags);
+#define LF(P)                                                                             \
+  hipLaunchKernelGGL((k_chains_flat<P>), dim3((int)blocks), dim3(kBlock), 0, stream, b,     \
+                     seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags)
+  switch (tn.chains_pass) {
+    case 2: LF(2); break;
+    case 8: LF(8); break;
+    case 4: LF(4); break;
+    default: LF(2); break;
+  }
+#undef LF
   return check_launch();
 }
 

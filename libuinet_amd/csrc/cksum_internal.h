@@ -9,6 +9,15 @@
 
 namespace uinet {
 
+// Process-wide performance knobs (uinet_cksum_set_tuning); seeded from the
+// environment on first use.  0 = "use the kernel's default".
+struct Tuning {
+  int blocks_per_cu;   // grid-stride width
+  int chains_variant;  // 0 flat, 1 serial
+  int chains_pass;     // 2, 4, 8
+};
+const Tuning& tuning();
+
 // Records the HIP error (if any) of the last launch on this thread and maps
 // it to a UINET_CKSUM_* code.
 int check_launch();

@@ -111,12 +111,8 @@ int grid_for(uint32_t n, int g, int bpc) {
 // strided kernel has no descriptors and prefers one packet per group (no
 // cap).  UINET_CKSUM_BLOCKS_PER_CU overrides every kernel's default.
 int blocks_per_cu(int dflt) {
-  static int v = [] {
-    const char* e = getenv("UINET_CKSUM_BLOCKS_PER_CU");
-    const int x = e ? atoi(e) : 0;
-    return (x > 0 && x <= 4096) ? x : 0;
-  }();
-  return v ? v : dflt;
+  const int v = tuning().blocks_per_cu;
+  return v > 0 ? v : dflt;
 }
 
 int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
@@ -124,7 +120,7 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
                  uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = pick_geometry(len_hint);
-  const int grid = grid_for(n, geo.g, 64);
+  const int grid = grid_for(n, geo.g, 128);
 #define L(G, U)                                                                    \
   hipLaunchKernelGGL((k_spans<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,  \
                      static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, out, \

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of engine tuning variants in ONE process (so DVFS and
+device-to-device spread hit every variant alike).
+
+  python tools/ab.py --config 3 --variants 'chains_pass=2' 'chains_pass=4' 'chains_pass=8'
+
+Each variant is a comma list of key=value pairs for uinet_cksum_set_tuning.
+Prints one JSON object: per variant the median / min kernel ms and GB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="2")
+    ap.add_argument("--api", default="spans")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--launches", type=int, default=10)
+    ap.add_argument("--variants", nargs="+", required=True)
+    a = ap.parse_args()
+    import torch
+
+    import bench
+    import libuinet_amd as u
+
+    w = bench.build_workload(a.config, None, 0)
+    out = torch.empty(w["n"], dtype=torch.uint16, device="cuda")
+    s = torch.cuda.current_stream()
+    launch = bench.make_launch(a.config, w, a.api, out)
+    variants = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(",") if kv)
+                for v in a.variants]
+    times = {i: [] for i in range(len(variants))}
+    ref = None
+    for r in range(a.rounds):
+        for i, v in enumerate(variants):
+            for k, val in v.items():
+                u.set_tuning(k, val)
+            launch(s)  # warm
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = out.clone()
+            elif not torch.equal(out, ref):
+                raise SystemExit(f"variant {a.variants[i]} changed results")
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(a.launches):
+                launch(s)
+            e1.record(s)
+            e1.synchronize()
+            times[i].append(e0.elapsed_time(e1) / a.launches)
+    res = {}
+    for i, v in enumerate(a.variants):
+        t = times[i]
+        res[v] = {"median_ms": round(statistics.median(t), 5), "min_ms": round(min(t), 5),
+                  "GBps_median": round(w["bytes"] / (statistics.median(t) * 1e-3) / 1e9, 1)}
+    print(json.dumps({"config": a.config, "api": a.api, "results": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
