@@ -167,6 +167,16 @@ int in_cksum_pseudo_header_batch(struct mbuf *const *m, const int *plen,
     const uint8_t *protonum, uint16_t *out, int n);
 int in_cksum_hdr_batch(const struct ip *const *ip, unsigned int *out, int n);
 
+/* Zero-copy host regions.  Register the host memory that holds packet data
+ * (the netmap ring buffers, uinet_if_netmap_host.c:153; the UMA slabs behind
+ * mbufs and clusters, uinet_vm_kern.c:48-51) once; a host-mbuf batch whose
+ * bytes all lie in registered regions is then folded in place by the GPU over
+ * PCIe -- the host only walks the chains, it copies no packet bytes.  Other
+ * batches are staged through pinned memory as before.  Regions must not
+ * overlap; memory that is already pinned (hipHostMalloc) is accepted as is. */
+int uinet_cksum_register_host(void *base, size_t len);
+int uinet_cksum_unregister_host(void *base);
+
 #if defined(__GNUC__)
 #pragma GCC visibility pop
 #endif

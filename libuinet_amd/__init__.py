@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "uinet_cksum_version", "uinet_cksum_strerror", "uinet_cksum_last_hip_error",
     "uinet_cksum_device_ok", "uinet_cksum_set_tuning", "uinet_cksum_spans", "uinet_cksum_strided", "uinet_cksum_chains",
     "in_cksum_skip_batch", "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch",
+    "uinet_cksum_register_host", "uinet_cksum_unregister_host",
 )
 
 
@@ -97,6 +98,8 @@ def lib() -> ctypes.CDLL:
         "in_cksum_skip_batch": (_i32, [_vp, _vp, _vp, _vp, _i32]),
         "in_cksum_pseudo_header_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32]),
         "in_cksum_hdr_batch": (_i32, [_vp, _vp, _i32]),
+        "uinet_cksum_register_host": (_i32, [_vp, ctypes.c_size_t]),
+        "uinet_cksum_unregister_host": (_i32, [_vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -171,6 +174,17 @@ def in_cksum_pseudo_header_batch(heads, plen, off0, src, dst, proto) -> np.ndarr
     _check("in_cksum_pseudo_header_batch",
            lib().in_cksum_pseudo_header_batch(_ptr(heads), *[_ptr(a) for a in arrs], _ptr(out), n))
     return out
+
+
+def register_host(buf: np.ndarray) -> None:
+    """uinet_cksum_register_host over a host buffer: batches whose bytes lie in
+    it are folded in place over PCIe (zero-copy)."""
+    _check("uinet_cksum_register_host",
+           lib().uinet_cksum_register_host(buf.ctypes.data, buf.nbytes))
+
+
+def unregister_host(buf: np.ndarray) -> None:
+    _check("uinet_cksum_unregister_host", lib().uinet_cksum_unregister_host(buf.ctypes.data))
 
 
 def in_cksum_hdr_batch(ips) -> np.ndarray:

@@ -23,6 +23,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "cksum_internal.h"
@@ -122,7 +124,7 @@ int ctx_reserve(Ctx& c, size_t bytes, size_t nout) {
     c.h_buf = nullptr;
     c.d_buf = nullptr;
     c.h_cap = c.d_cap = 0;
-    int rc = record_hip(hipHostMalloc((void**)&c.h_buf, cap, hipHostMallocDefault));
+    int rc = record_hip(hipHostMalloc((void**)&c.h_buf, cap, hipHostMallocMapped));
     if (rc) return rc;
     rc = record_hip(hipMalloc((void**)&c.d_buf, cap));
     if (rc) return rc;
@@ -136,7 +138,7 @@ int ctx_reserve(Ctx& c, size_t bytes, size_t nout) {
     c.h_out = nullptr;
     c.d_out = nullptr;
     c.out_cap = 0;
-    int rc = record_hip(hipHostMalloc((void**)&c.h_out, cap * 2, hipHostMallocDefault));
+    int rc = record_hip(hipHostMalloc((void**)&c.h_out, cap * 2, hipHostMallocMapped));
     if (rc) return rc;
     rc = record_hip(hipMalloc((void**)&c.d_out, cap * 2));
     if (rc) return rc;
@@ -155,7 +157,7 @@ struct Piece {
 // One packet as the reference walks it: the in-order pieces whose bytes are
 // summed, the logical parity of the first summed byte, and the seed.
 struct PacketWalk {
-  std::vector<Piece> pieces;
+  std::vector<Piece>* out = nullptr;  // pieces are appended here
   uint64_t bytes = 0;
   long clen = 0;    // logical bytes consumed (may go negative, see below)
   long remain = 0;  // bytes still wanted
@@ -163,7 +165,6 @@ struct PacketWalk {
   bool have_first = false;
 
   void reset(long want) {
-    pieces.clear();
     bytes = 0;
     clen = 0;
     remain = want;
@@ -182,7 +183,7 @@ struct PacketWalk {
         have_first = true;
         first_clen = clen;
       }
-      pieces.push_back({addr, (uint32_t)mlen});
+      out->push_back({addr, (uint32_t)mlen});
       bytes += (uint64_t)mlen;
     }
     clen += mlen;
@@ -231,8 +232,53 @@ Layout layout_for(size_t n) {
   return L;
 }
 
-// Pack the walked packets, run the span kernel, copy results back.
-// `walk(i, pw)` fills pw for packet i and returns its seed.
+// ---- registered host regions (zero-copy) ------------------------------------
+//
+// Memory registered with uinet_cksum_register_host (netmap rings, UMA slabs)
+// is mapped into the GPU's address space; a batch whose pieces all lie in
+// registered regions is folded in place over PCIe -- the host only walks the
+// chains and writes 12-byte descriptors, it never copies packet bytes.
+
+struct Region {
+  uintptr_t base, end;
+  intptr_t delta;  // device address - host address
+  bool owned;      // registered by us (unregister on removal)
+};
+
+std::mutex g_reg_mu;
+std::vector<Region> g_regions;  // sorted by base, non-overlapping
+
+// Device address of [p, p + n) if it lies inside one registered region.
+bool device_addr(const std::vector<Region>& regs, const uint8_t* p, uint32_t n,
+                 uint64_t* dev) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  size_t lo = 0, hi = regs.size();
+  while (lo < hi) {
+    const size_t mid = (lo + hi) / 2;
+    if (regs[mid].base <= a) lo = mid + 1; else hi = mid;
+  }
+  if (lo == 0) return false;
+  const Region& r = regs[lo - 1];
+  if (a < r.base || a + n > r.end) return false;
+  *dev = (uint64_t)(a + r.delta);
+  return true;
+}
+
+// ---- walked batches -------------------------------------------------------------
+
+// Per-thread scratch for a walked batch, reused across calls: the pieces of
+// every packet back to back (pk_first[i] .. pk_first[i+1]).
+struct Batch {
+  std::vector<Piece> pieces;
+  std::vector<uint32_t> pk_first, seed;
+  std::vector<uint8_t> par;
+  PacketWalk w;
+};
+thread_local Batch t_batch;
+
+// Walk every packet (`walk(i, pw)` fills pw and returns the packet's seed),
+// then either fold the pieces in place (all registered, even start parity)
+// or pack them into pinned staging; one launch either way.
 template <typename WalkFn>
 int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, WalkFn walk) {
   if (n < 0) return UINET_CKSUM_EINVAL;
@@ -241,53 +287,105 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   int rc = ctx_ready(c);
   if (rc) return rc;
 
-  // Pass 1: walk, remember pieces (pointer chasing happens once).
-  std::vector<PacketWalk> walks((size_t)n);
-  std::vector<uint32_t> seeds((size_t)n);
-  uint64_t total = 0;
+  Batch& B = t_batch;
+  B.pieces.clear();
+  B.w.out = &B.pieces;
+  B.pk_first.resize((size_t)n + 1);
+  B.seed.resize((size_t)n);
+  B.par.resize((size_t)n);
+  uint64_t total = 0, packed = 0;
+  bool odd_start = false;
   for (int i = 0; i < n; i++) {
-    seeds[(size_t)i] = walk(i, walks[(size_t)i]);
-    total += (walks[(size_t)i].bytes + 15) & ~uint64_t(15);
+    B.pk_first[(size_t)i] = (uint32_t)B.pieces.size();
+    B.seed[(size_t)i] = walk(i, B.w);
+    if (B.w.bytes > 0xffffffffull) return UINET_CKSUM_EINVAL;
+    B.par[(size_t)i] = (uint8_t)(B.w.first_clen & 1);
+    odd_start |= B.par[(size_t)i] != 0;
+    total += B.w.bytes;
+    packed += (B.w.bytes + 15) & ~uint64_t(15);
   }
-  const Layout L = layout_for((size_t)n);
-  rc = ctx_reserve(c, L.data_o + total + 16, (size_t)n);
-  if (rc) return rc;
-
-  // Pass 2: pack descriptors and bytes into pinned staging.
-  uint64_t* off = reinterpret_cast<uint64_t*>(c.h_buf + L.off_o);
-  uint32_t* len = reinterpret_cast<uint32_t*>(c.h_buf + L.len_o);
-  uint32_t* seed = reinterpret_cast<uint32_t*>(c.h_buf + L.seed_o);
-  uint8_t* par = c.h_buf + L.par_o;
-  uint64_t cur = 0;
-  uint32_t max_len = 0;
-  for (int i = 0; i < n; i++) {
-    const PacketWalk& w = walks[(size_t)i];
-    if (w.bytes > 0xffffffffull) return UINET_CKSUM_EINVAL;
-    off[i] = cur;
-    len[i] = (uint32_t)w.bytes;
-    seed[i] = seeds[(size_t)i];
-    par[i] = (uint8_t)(w.first_clen & 1);
-    uint8_t* dst = c.h_buf + L.data_o + cur;
-    for (const Piece& p : w.pieces) {
-      memcpy(dst, p.p, p.n);
-      dst += p.n;
-    }
-    cur += (w.bytes + 15) & ~uint64_t(15);
-    if (len[i] > max_len) max_len = len[i];
-  }
-  const size_t image = L.data_o + cur;
-
-  rc = record_hip(hipMemcpyAsync(c.d_buf, c.h_buf, image, hipMemcpyHostToDevice, c.stream));
-  if (rc) return rc;
+  B.pk_first[(size_t)n] = (uint32_t)B.pieces.size();
+  const size_t np = B.pieces.size();
   const uint32_t mean = (uint32_t)(total / (uint64_t)n);
-  rc = launch_spans(c.d_buf + L.data_o, reinterpret_cast<const uint64_t*>(c.d_buf + L.off_o),
-                    reinterpret_cast<const uint32_t*>(c.d_buf + L.len_o),
-                    reinterpret_cast<const uint32_t*>(c.d_buf + L.seed_o), c.d_buf + L.par_o,
-                    c.d_out, (uint32_t)n, flags, mean ? mean : 1, c.stream);
-  if (rc) return rc;
-  rc = record_hip(hipMemcpyAsync(c.h_out, c.d_out, (size_t)n * 2, hipMemcpyDeviceToHost,
-                                 c.stream));
-  if (rc) return rc;
+
+  // Zero-copy when every piece is in a registered region.  (The chain kernel
+  // counts logical parity from each packet's first byte, so odd starts --
+  // in_cksum_hdr at an odd address, out-of-contract negative pieces -- take
+  // the staging path, which carries a parity per packet.)
+  bool zero_copy = !odd_start && np > 0;
+  if (zero_copy) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    zero_copy = !g_regions.empty();
+    // descriptors: seg_off u64[np] | seg_len u32[np] | pkt_seg u32[n+1] | seed u32[n]
+    const size_t need = 8 * np + 4 * np + 4 * ((size_t)n + 1) + 4 * (size_t)n + 64;
+    if (zero_copy && (rc = ctx_reserve(c, need, (size_t)n)) != 0) return rc;
+    uint64_t* so = reinterpret_cast<uint64_t*>(c.h_buf);
+    for (size_t k = 0; zero_copy && k < np; k++)
+      zero_copy = device_addr(g_regions, B.pieces[k].p, B.pieces[k].n, &so[k]);
+  }
+  if (zero_copy) {
+    uint64_t* so = reinterpret_cast<uint64_t*>(c.h_buf);
+    uint32_t* sl = reinterpret_cast<uint32_t*>(c.h_buf + 8 * np);
+    uint32_t* ps = sl + np;
+    uint32_t* sd = ps + n + 1;
+    uint64_t lo_addr = so[0];
+    for (size_t k = 0; k < np; k++) {
+      sl[k] = B.pieces[k].n;
+      lo_addr = so[k] < lo_addr ? so[k] : lo_addr;
+    }
+    for (size_t k = 0; k < np; k++) so[k] -= lo_addr;  // offsets from the lowest piece
+    memcpy(ps, B.pk_first.data(), 4 * ((size_t)n + 1));
+    memcpy(sd, B.seed.data(), 4 * (size_t)n);
+    // Descriptors and results stay in pinned host memory too: the kernel
+    // reads/writes them over PCIe, so the batch costs one launch, no copies.
+    void* dd = nullptr;
+    void* dout = nullptr;
+    rc = record_hip(hipHostGetDevicePointer(&dd, c.h_buf, 0));
+    if (rc) return rc;
+    rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
+    if (rc) return rc;
+    uint8_t* d = static_cast<uint8_t*>(dd);
+    rc = launch_chains(reinterpret_cast<const void*>(lo_addr), reinterpret_cast<uint64_t*>(d),
+                       reinterpret_cast<uint32_t*>(d + 8 * np),
+                       reinterpret_cast<uint32_t*>(d + 12 * np), nullptr, nullptr,
+                       reinterpret_cast<uint32_t*>(d + 12 * np + 4 * ((size_t)n + 1)),
+                       static_cast<uint16_t*>(dout), (uint32_t)n, flags,
+                       (uint32_t)(total / np), c.stream);
+    if (rc) return rc;
+  } else {
+    const Layout L = layout_for((size_t)n);
+    rc = ctx_reserve(c, L.data_o + packed + 16, (size_t)n);
+    if (rc) return rc;
+    uint64_t* off = reinterpret_cast<uint64_t*>(c.h_buf + L.off_o);
+    uint32_t* len = reinterpret_cast<uint32_t*>(c.h_buf + L.len_o);
+    uint32_t* seed = reinterpret_cast<uint32_t*>(c.h_buf + L.seed_o);
+    uint8_t* par = c.h_buf + L.par_o;
+    uint64_t cur = 0;
+    for (int i = 0; i < n; i++) {
+      off[i] = cur;
+      seed[i] = B.seed[(size_t)i];
+      par[i] = B.par[(size_t)i];
+      uint8_t* dst = c.h_buf + L.data_o + cur;
+      uint64_t bytes = 0;
+      for (uint32_t k = B.pk_first[(size_t)i]; k < B.pk_first[(size_t)i + 1]; k++) {
+        memcpy(dst + bytes, B.pieces[k].p, B.pieces[k].n);
+        bytes += B.pieces[k].n;
+      }
+      len[i] = (uint32_t)bytes;
+      cur += (bytes + 15) & ~uint64_t(15);
+    }
+    const size_t image = L.data_o + cur;
+    rc = record_hip(hipMemcpyAsync(c.d_buf, c.h_buf, image, hipMemcpyHostToDevice, c.stream));
+    if (rc) return rc;
+    rc = launch_spans(c.d_buf + L.data_o, reinterpret_cast<const uint64_t*>(c.d_buf + L.off_o),
+                      reinterpret_cast<const uint32_t*>(c.d_buf + L.len_o),
+                      reinterpret_cast<const uint32_t*>(c.d_buf + L.seed_o), c.d_buf + L.par_o,
+                      c.d_out, (uint32_t)n, flags, mean ? mean : 1, c.stream);
+    if (rc) return rc;
+    rc = record_hip(hipMemcpyAsync(c.h_out, c.d_out, (size_t)n * 2, hipMemcpyDeviceToHost,
+                                   c.stream));
+    if (rc) return rc;
+  }
   rc = record_hip(hipStreamSynchronize(c.stream));
   if (rc) return rc;
   for (int i = 0; i < n; i++) {
@@ -324,6 +422,46 @@ const char* uinet_cksum_strerror(int code) {
 }
 
 int uinet_cksum_last_hip_error(void) { return t_last_hip; }
+
+int uinet_cksum_register_host(void* base, size_t len) {
+  if (!base || len == 0) return UINET_CKSUM_EINVAL;
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base), e = b + len;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (const Region& r : g_regions)
+    if (b < r.end && r.base < e) return UINET_CKSUM_EINVAL;  // overlaps
+  bool owned = true;
+  hipError_t he = hipHostRegister(base, len, hipHostRegisterMapped);
+  if (he == hipErrorHostMemoryAlreadyRegistered) {  // e.g. hipHostMalloc'd / torch-pinned
+    (void)hipGetLastError();
+    owned = false;
+  } else if (he != hipSuccess) {
+    return record_hip(he);
+  }
+  void* dev = nullptr;
+  int rc = record_hip(hipHostGetDevicePointer(&dev, base, 0));
+  if (rc) {
+    if (owned) (void)hipHostUnregister(base);
+    return rc;
+  }
+  Region r{b, e, (intptr_t)(reinterpret_cast<uintptr_t>(dev) - b), owned};
+  g_regions.insert(std::upper_bound(g_regions.begin(), g_regions.end(), r,
+                                    [](const Region& x, const Region& y) { return x.base < y.base; }),
+                   r);
+  return UINET_CKSUM_OK;
+}
+
+int uinet_cksum_unregister_host(void* base) {
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (size_t i = 0; i < g_regions.size(); i++) {
+    if (g_regions[i].base == b) {
+      const bool owned = g_regions[i].owned;
+      g_regions.erase(g_regions.begin() + (long)i);
+      return owned ? record_hip(hipHostUnregister(base)) : UINET_CKSUM_OK;
+    }
+  }
+  return UINET_CKSUM_EINVAL;
+}
 
 int uinet_cksum_set_tuning(const char* key, int value) {
   if (!key) return UINET_CKSUM_EINVAL;

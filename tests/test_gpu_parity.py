@@ -223,6 +223,55 @@ def test_pcap_kat_gpu(torch_dev, pcap_frames):
     assert not u.in_cksum_pseudo_header_batch(ch.heads, plen, hl, src, dst, 6).any()
 
 
+def test_zero_copy_registered_arena(torch_dev, arena, golden):
+    """Registered host memory: the batches are folded in place over PCIe by
+    the chain kernel (no staging copy) -- same golden results."""
+    u.register_host(arena)
+    try:
+        g = golden("skip")
+        ch = MbufChains(arena, g["seg_off"], g["seg_len"], g["pkt_seg"])
+        np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, g["len"], g["skip"]),
+                                      g["expected"])
+        g = golden("pseudo")
+        ch = MbufChains(arena, g["seg_off"], g["seg_len"], g["pkt_seg"])
+        got = u.in_cksum_pseudo_header_batch(ch.heads, g["plen"], g["off0"], g["src"], g["dst"],
+                                             g["proto"])
+        np.testing.assert_array_equal(got, g["expected"])
+        g = golden("hdr")
+        even = (g["off"] % 2) == 0  # odd header addresses take the staging path
+        ips = arena.ctypes.data + g["off"].astype(np.uint64)
+        np.testing.assert_array_equal(u.in_cksum_hdr_batch(ips[even]), g["expected"][even])
+        np.testing.assert_array_equal(u.in_cksum_hdr_batch(ips), g["expected"])
+        g = golden("configs")
+        ch = MbufChains(arena, g["c3_seg_off"], g["c3_seg_len"], g["c3_pkt_seg"])
+        np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, g["c3_len"], 20),
+                                      g["c3_expected"])
+        with pytest.raises(u.CksumError):
+            u.register_host(arena)  # overlapping registration is refused
+    finally:
+        u.unregister_host(arena)
+
+
+def test_zero_copy_partial_registration(torch_dev, ora):
+    """Pieces outside registered memory send the batch through staging."""
+    rng = np.random.default_rng(81)
+    arena = rand_arena(1 << 20, 81)
+    half = arena[: 1 << 19]
+    seg_off, seg_len, pkt_seg = random_chain_layout(rng, 3000, arena.size)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1])
+    want = ora.skip_batch(ch.heads, tot, 0)
+    u.register_host(half)
+    try:
+        np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, tot, 0), want)
+        inside = np.array([seg_off[pkt_seg[i]:pkt_seg[i + 1]].max(initial=0) < (1 << 19) - 300
+                           for i in range(ch.n)])
+        np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads[inside], tot[inside], 0),
+                                      want[inside])
+    finally:
+        u.unregister_host(half)
+
+
 def test_host_batch_threads(torch_dev, ora):
     """Concurrent callers (RX threads + TX app threads)."""
     rng = np.random.default_rng(77)
