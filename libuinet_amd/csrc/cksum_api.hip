@@ -14,7 +14,9 @@
 //
 // Threading: the reference checksum is fully reentrant; here
 // every calling thread gets its own stream and staging buffers (thread_local),
-// so concurrent RX/TX threads never share state and take no locks.
+// so concurrent RX/TX threads never share device state.  A large host-mbuf
+// batch is walked and packed by the host pool (host_pool.h); a batch that
+// finds the pool in use by another thread does that work itself.
 #include <hip/hip_runtime.h>
 
 #include <stddef.h>
@@ -25,9 +27,11 @@
 
 #include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "cksum_internal.h"
+#include "host_pool.h"
 
 namespace uinet {
 
@@ -57,7 +61,8 @@ int check_launch() { return record_hip(hipGetLastError()); }
 
 static Tuning& tuning_rw() {
   static Tuning t = [] {
-    Tuning x{0, 0, 2};
+    const unsigned hw = std::thread::hardware_concurrency();
+    Tuning x{0, 0, 2, (int)std::min(8u, hw ? hw : 1u)};
     if (const char* e = getenv("UINET_CKSUM_BLOCKS_PER_CU")) {
       const int v = atoi(e);
       x.blocks_per_cu = (v > 0 && v <= 4096) ? v : 0;
@@ -66,6 +71,10 @@ static Tuning& tuning_rw() {
     if (const char* e = getenv("UINET_CKSUM_CHAINS_PASS")) {
       const int v = atoi(e);
       if (v == 2 || v == 4 || v == 8) x.chains_pass = v;
+    }
+    if (const char* e = getenv("UINET_CKSUM_HOST_THREADS")) {
+      const int v = atoi(e);
+      if (v >= 1 && v <= 64) x.host_threads = v;
     }
     return x;
   }();
@@ -265,20 +274,54 @@ bool device_addr(const std::vector<Region>& regs, const uint8_t* p, uint32_t n,
 }
 
 // ---- walked batches -------------------------------------------------------------
+//
+// A batch runs in three phases.  (1) Every packet is walked like the reference
+// walks it; packets are split into chunks of consecutive packets that the host
+// pool walks in parallel, each chunk into its own piece list.  (2) A serial
+// prefix over the chunks places them.  (3) The chunks, again in parallel,
+// either write chain descriptors that point into registered memory (zero-copy:
+// the kernel folds the bytes in place over PCIe) or pack the bytes into pinned
+// staging for one H2D copy and one span launch.
 
-// Per-thread scratch for a walked batch, reused across calls: the pieces of
-// every packet back to back (pk_first[i] .. pk_first[i+1]).
-struct Batch {
+struct Chunk {
   std::vector<Piece> pieces;
-  std::vector<uint32_t> pk_first, seed;
-  std::vector<uint8_t> par;
   PacketWalk w;
+  int i0 = 0, i1 = 0;          // packets [i0, i1)
+  uint64_t total = 0, packed = 0;
+  uint32_t first_piece = 0;    // global index of pieces[0]
+  uint64_t pack_base = 0;      // staging offset of packet i0
+  bool odd = false, too_big = false, unmapped = false;
+};
+
+// Per-thread scratch, reused across calls.
+struct Batch {
+  std::vector<Chunk> chunks;
+  std::vector<uint32_t> pk_first, seed, bytes;  // pk_first is chunk-local
+  std::vector<uint8_t> par;
 };
 thread_local Batch t_batch;
 
+constexpr int kChunkMin = 1024;  // packets; below this one thread walks
+
+// Device address of [p, p + n) with a one-entry cache of the last region hit
+// (consecutive pieces almost always share a region).
+inline bool device_addr_cached(const std::vector<Region>& regs, const uint8_t* p, uint32_t n,
+                               const Region*& last, uint64_t* dev) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  if (last && a >= last->base && a + n <= last->end) {
+    *dev = (uint64_t)(a + last->delta);
+    return true;
+  }
+  if (!device_addr(regs, p, n, dev)) return false;
+  last = &*(std::upper_bound(regs.begin(), regs.end(), a,
+                             [](uintptr_t x, const Region& r) { return x < r.base; }) -
+            1);
+  return true;
+}
+
 // Walk every packet (`walk(i, pw)` fills pw and returns the packet's seed),
-// then either fold the pieces in place (all registered, even start parity)
-// or pack them into pinned staging; one launch either way.
+// then fold the pieces in place (all registered, even start parity) or pack
+// them into pinned staging; one launch either way.
 template <typename WalkFn>
 int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, WalkFn walk) {
   if (n < 0) return UINET_CKSUM_EINVAL;
@@ -287,55 +330,101 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   int rc = ctx_ready(c);
   if (rc) return rc;
 
+  const int threads = tuning().host_threads;
+  int cs = (n + threads * 4 - 1) / (threads * 4);
+  if (cs < kChunkMin) cs = kChunkMin;
+  const int nch = (n + cs - 1) / cs;
   Batch& B = t_batch;
-  B.pieces.clear();
-  B.w.out = &B.pieces;
+  if ((int)B.chunks.size() < nch) B.chunks.resize((size_t)nch);
   B.pk_first.resize((size_t)n + 1);
   B.seed.resize((size_t)n);
+  B.bytes.resize((size_t)n);
   B.par.resize((size_t)n);
-  uint64_t total = 0, packed = 0;
+  HostPool& pool = host_pool();
+
+  // (1) walk
+  pool.run(nch, threads, [&](int j) {
+    Chunk& C = B.chunks[(size_t)j];
+    C.i0 = j * cs;
+    C.i1 = std::min(n, C.i0 + cs);
+    C.pieces.clear();
+    C.w.out = &C.pieces;
+    C.total = C.packed = 0;
+    C.odd = C.too_big = C.unmapped = false;
+    for (int i = C.i0; i < C.i1; i++) {
+      B.pk_first[(size_t)i] = (uint32_t)C.pieces.size();
+      B.seed[(size_t)i] = walk(i, C.w);
+      const uint64_t nb = C.w.bytes;
+      C.too_big |= nb > 0xffffffffull;
+      B.bytes[(size_t)i] = (uint32_t)nb;
+      B.par[(size_t)i] = (uint8_t)(C.w.first_clen & 1);
+      C.odd |= B.par[(size_t)i] != 0;
+      C.total += nb;
+      C.packed += (nb + 15) & ~uint64_t(15);
+    }
+  });
+
+  // (2) place the chunks
+  uint64_t total = 0, packed = 0, np64 = 0;
   bool odd_start = false;
-  for (int i = 0; i < n; i++) {
-    B.pk_first[(size_t)i] = (uint32_t)B.pieces.size();
-    B.seed[(size_t)i] = walk(i, B.w);
-    if (B.w.bytes > 0xffffffffull) return UINET_CKSUM_EINVAL;
-    B.par[(size_t)i] = (uint8_t)(B.w.first_clen & 1);
-    odd_start |= B.par[(size_t)i] != 0;
-    total += B.w.bytes;
-    packed += (B.w.bytes + 15) & ~uint64_t(15);
+  for (int j = 0; j < nch; j++) {
+    Chunk& C = B.chunks[(size_t)j];
+    if (C.too_big) return UINET_CKSUM_EINVAL;
+    C.first_piece = (uint32_t)np64;
+    C.pack_base = packed;
+    np64 += C.pieces.size();
+    total += C.total;
+    packed += C.packed;
+    odd_start |= C.odd;
   }
-  B.pk_first[(size_t)n] = (uint32_t)B.pieces.size();
-  const size_t np = B.pieces.size();
+  if (np64 > 0xffffffffull) return UINET_CKSUM_EINVAL;
+  const size_t np = (size_t)np64;
   const uint32_t mean = (uint32_t)(total / (uint64_t)n);
 
-  // Zero-copy when every piece is in a registered region.  (The chain kernel
-  // counts logical parity from each packet's first byte, so odd starts --
-  // in_cksum_hdr at an odd address, out-of-contract negative pieces -- take
+  // (3a) zero-copy when every piece is in a registered region.  (The chain
+  // kernel counts logical parity from each packet's first byte, so odd starts
+  // -- in_cksum_hdr at an odd address, out-of-contract negative pieces -- take
   // the staging path, which carries a parity per packet.)
   bool zero_copy = !odd_start && np > 0;
+  uint64_t lo_addr = 0;
   if (zero_copy) {
     std::lock_guard<std::mutex> g(g_reg_mu);
     zero_copy = !g_regions.empty();
     // descriptors: seg_off u64[np] | seg_len u32[np] | pkt_seg u32[n+1] | seed u32[n]
     const size_t need = 8 * np + 4 * np + 4 * ((size_t)n + 1) + 4 * (size_t)n + 64;
     if (zero_copy && (rc = ctx_reserve(c, need, (size_t)n)) != 0) return rc;
-    uint64_t* so = reinterpret_cast<uint64_t*>(c.h_buf);
-    for (size_t k = 0; zero_copy && k < np; k++)
-      zero_copy = device_addr(g_regions, B.pieces[k].p, B.pieces[k].n, &so[k]);
+    if (zero_copy) {
+      lo_addr = ~0ull;
+      for (const Region& r : g_regions)
+        lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
+      uint64_t* so = reinterpret_cast<uint64_t*>(c.h_buf);
+      uint32_t* sl = reinterpret_cast<uint32_t*>(c.h_buf + 8 * np);
+      uint32_t* ps = sl + np;
+      uint32_t* sd = ps + n + 1;
+      const std::vector<Region>& regs = g_regions;
+      pool.run(nch, threads, [&](int j) {
+        Chunk& C = B.chunks[(size_t)j];
+        const Region* last = nullptr;
+        const size_t g0 = C.first_piece;
+        for (size_t k = 0; k < C.pieces.size(); k++) {
+          uint64_t dev;
+          if (!device_addr_cached(regs, C.pieces[k].p, C.pieces[k].n, last, &dev)) {
+            C.unmapped = true;
+            return;
+          }
+          so[g0 + k] = dev - lo_addr;
+          sl[g0 + k] = C.pieces[k].n;
+        }
+        for (int i = C.i0; i < C.i1; i++) {
+          ps[i] = C.first_piece + B.pk_first[(size_t)i];
+          sd[i] = B.seed[(size_t)i];
+        }
+      });
+      ps[n] = (uint32_t)np;
+      for (int j = 0; j < nch; j++) zero_copy &= !B.chunks[(size_t)j].unmapped;
+    }
   }
   if (zero_copy) {
-    uint64_t* so = reinterpret_cast<uint64_t*>(c.h_buf);
-    uint32_t* sl = reinterpret_cast<uint32_t*>(c.h_buf + 8 * np);
-    uint32_t* ps = sl + np;
-    uint32_t* sd = ps + n + 1;
-    uint64_t lo_addr = so[0];
-    for (size_t k = 0; k < np; k++) {
-      sl[k] = B.pieces[k].n;
-      lo_addr = so[k] < lo_addr ? so[k] : lo_addr;
-    }
-    for (size_t k = 0; k < np; k++) so[k] -= lo_addr;  // offsets from the lowest piece
-    memcpy(ps, B.pk_first.data(), 4 * ((size_t)n + 1));
-    memcpy(sd, B.seed.data(), 4 * (size_t)n);
     // Descriptors and results stay in pinned host memory too: the kernel
     // reads/writes them over PCIe, so the batch costs one launch, no copies.
     void* dd = nullptr;
@@ -353,6 +442,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
                        (uint32_t)(total / np), c.stream);
     if (rc) return rc;
   } else {
+    // (3b) staging
     const Layout L = layout_for((size_t)n);
     rc = ctx_reserve(c, L.data_o + packed + 16, (size_t)n);
     if (rc) return rc;
@@ -360,22 +450,27 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     uint32_t* len = reinterpret_cast<uint32_t*>(c.h_buf + L.len_o);
     uint32_t* seed = reinterpret_cast<uint32_t*>(c.h_buf + L.seed_o);
     uint8_t* par = c.h_buf + L.par_o;
-    uint64_t cur = 0;
-    for (int i = 0; i < n; i++) {
-      off[i] = cur;
-      seed[i] = B.seed[(size_t)i];
-      par[i] = B.par[(size_t)i];
-      uint8_t* dst = c.h_buf + L.data_o + cur;
-      uint64_t bytes = 0;
-      for (uint32_t k = B.pk_first[(size_t)i]; k < B.pk_first[(size_t)i + 1]; k++) {
-        memcpy(dst + bytes, B.pieces[k].p, B.pieces[k].n);
-        bytes += B.pieces[k].n;
+    uint8_t* data = c.h_buf + L.data_o;
+    pool.run(nch, threads, [&](int j) {
+      const Chunk& C = B.chunks[(size_t)j];
+      uint64_t cur = C.pack_base;
+      uint32_t k = 0;
+      for (int i = C.i0; i < C.i1; i++) {
+        off[i] = cur;
+        seed[i] = B.seed[(size_t)i];
+        par[i] = B.par[(size_t)i];
+        len[i] = B.bytes[(size_t)i];
+        const uint32_t k1 = i + 1 < C.i1 ? B.pk_first[(size_t)i + 1] : (uint32_t)C.pieces.size();
+        uint8_t* dst = data + cur;
+        for (; k < k1; k++) {
+          memcpy(dst, C.pieces[k].p, C.pieces[k].n);
+          dst += C.pieces[k].n;
+        }
+        cur += ((uint64_t)B.bytes[(size_t)i] + 15) & ~uint64_t(15);
       }
-      len[i] = (uint32_t)bytes;
-      cur += (bytes + 15) & ~uint64_t(15);
-    }
-    const size_t image = L.data_o + cur;
-    rc = record_hip(hipMemcpyAsync(c.d_buf, c.h_buf, image, hipMemcpyHostToDevice, c.stream));
+    });
+    rc = record_hip(hipMemcpyAsync(c.d_buf, c.h_buf, L.data_o + packed, hipMemcpyHostToDevice,
+                                   c.stream));
     if (rc) return rc;
     rc = launch_spans(c.d_buf + L.data_o, reinterpret_cast<const uint64_t*>(c.d_buf + L.off_o),
                       reinterpret_cast<const uint32_t*>(c.d_buf + L.len_o),
@@ -472,6 +567,8 @@ int uinet_cksum_set_tuning(const char* key, int value) {
     t.chains_variant = value;
   } else if (!strcmp(key, "chains_pass") && (value == 2 || value == 4 || value == 8)) {
     t.chains_pass = value;
+  } else if (!strcmp(key, "host_threads") && value >= 1 && value <= 64) {
+    t.host_threads = value;
   } else {
     return UINET_CKSUM_EINVAL;
   }

@@ -15,6 +15,7 @@ struct Tuning {
   int blocks_per_cu;   // grid-stride width
   int chains_variant;  // 0 flat, 1 serial
   int chains_pass;     // 2, 4, 8
+  int host_threads;    // host-mbuf batch walk/pack threads, 1..64
 };
 const Tuning& tuning();
 

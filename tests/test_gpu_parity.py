@@ -425,3 +425,43 @@ def test_full_config5_jumbo(torch_dev, ora):
     np.testing.assert_array_equal(
         u.in_cksum_pseudo_header_batch(ch.heads, 8980, 20, src[:256], dst[:256], proto[:256]),
         want[:256])
+
+
+@pytest.mark.parametrize("host_threads", [1, 3, 8])
+def test_host_batch_chunked(torch_dev, ora, host_threads):
+    """Batches large enough to be walked/packed in chunks by the host pool
+    (staging and zero-copy), with concurrent callers contending for it."""
+    rng = np.random.default_rng(90 + host_threads)
+    arena = rand_arena(1 << 22, 90)
+    seg_off, seg_len, pkt_seg = random_chain_layout(rng, 24000, arena.size)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1])
+    skip = rng.integers(0, 40, ch.n).astype(np.int32)
+    want = ora.skip_batch(ch.heads, tot, skip)
+    u.set_tuning("host_threads", host_threads)
+    try:
+        np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, tot, skip), want)
+        u.register_host(arena)
+        try:
+            np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, tot, skip), want)
+            results, errors = {}, []
+
+            def worker(k):
+                try:
+                    sl = slice(k * 6000, (k + 1) * 6000)
+                    for _ in range(3):
+                        results[k] = u.in_cksum_skip_batch(ch.heads[sl], tot[sl], skip[sl])
+                except Exception as e:  # pragma: no cover
+                    errors.append(e)
+
+            th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            assert not errors
+            np.testing.assert_array_equal(np.concatenate([results[k] for k in range(4)]), want)
+        finally:
+            u.unregister_host(arena)
+    finally:
+        u.set_tuning("host_threads", 8)
