@@ -32,6 +32,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
+CHAIN_CONFIGS = ("3", "3tx", "5tso")
 
 
 def parse():
@@ -39,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", choices=["2", "2rx", "3", "5"], default="2",
+    ap.add_argument("--config", choices=["2", "2rx", "3", "3tx", "5", "5tso"], default="2",
                     help="BASELINE.json config shape (2 = the headline)")
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU")
     ap.add_argument("--api", choices=["spans", "strided"], default="spans")
@@ -76,6 +77,18 @@ def build_workload(cfg: str, n, rank: int):
         w["desc"] = (f"config3: {n:,} mixed 64/576/1500 B packets as {w['nseg']:,} chained "
                      f"1..256 B mbuf segments, in_cksum_skip(m,len,20)")
         w["hint"] = w["mean_seg"]
+    elif cfg in ("3tx", "5tso"):
+        w = W.materialize_device(W.chain_layout(cfg, n))
+        w["hint"] = w["mean_seg"]
+        n = w["n"]
+        if cfg == "3tx":
+            w["desc"] = (f"config3tx: {n:,} mixed 64/576/1500 B packets in the reference TX "
+                         f"shape (40-B header mbuf -> 4-KiB page-cluster slices, {w['nseg']:,} "
+                         f"segments), in_cksum_skip(m,len,20)")
+        else:
+            w["desc"] = (f"config5tso: {w['layout']['sends']:,} 1-MiB sends cut at MSS 8960 into "
+                         f"{n:,} segments (40-B header -> payload slice), "
+                         f"in_cksum_pseudo_header(m,20+seglen,20,src,dst,TCP)")
     else:
         n = n or 131072
         w = W.config5_device(n, rank=rank)
@@ -88,10 +101,10 @@ def build_workload(cfg: str, n, rank: int):
 def make_launch(cfg: str, w, api: str, out):
     import libuinet_amd as u
 
-    if cfg == "3":
+    if cfg in CHAIN_CONFIGS:
         return lambda s: u.cksum_chains(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"],
-                                        length=w["len"], skip=w["skip"], out=out,
-                                        len_hint=w["hint"], stream=s)
+                                        length=w["len"], skip=w["skip"], seed=w.get("seed"),
+                                        out=out, len_hint=w["hint"], stream=s)
     if api == "strided" and cfg in ("2", "2rx"):
         base = w["arena"][w["base"]:]
         return lambda s: u.cksum_strided(base, w["stride"], w["length"], w["n"], out=out, stream=s)
@@ -101,7 +114,7 @@ def make_launch(cfg: str, w, api: str, out):
 
 
 def kernel_name(cfg: str, api: str) -> str:
-    if cfg == "3":
+    if cfg in CHAIN_CONFIGS:
         return "k_chains"
     return "k_strided" if api == "strided" else "k_spans"
 
@@ -131,7 +144,13 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
         allowed = list(range(os.cpu_count() or 1))
     threads = max(1, min(threads, len(allowed)))
     cpus = allowed[:threads]
-    if cfg == "3":
+    if cfg == "5tso":
+        lay = w["layout"]
+        ch = MbufChains(host, lay["seg_off"], lay["seg_len"], lay["pkt_seg"])
+        args = (ch.heads, lay["plen"], 20, lay["src"], lay["dst"], 6)
+        timer = (lambda nt, cp, r: R.time_pseudo(*args, nthreads=nt, cpus=cp, reps=r)) if R else None
+        port = lambda: oracle.Oracle().pseudo_header_batch(*args)  # noqa: E731
+    elif cfg in ("3", "3tx"):
         lay = w["layout"]
         ch = MbufChains(host, lay["seg_off"], lay["seg_len"], lay["pkt_seg"])
         args = (ch.heads, lay["lens"], 20)
@@ -160,7 +179,7 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
     return {
         "value": round(gib / tn, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
         "sample": (f"{w['n']:,} packets ({gib:.3f} GiB algorithmic) of the benchmarked batch, "
-                   f"host copy as {'chained ' if cfg == '3' else ''}struct mbuf; best of 5 on "
+                   f"host copy as {'chained ' if cfg in CHAIN_CONFIGS else ''}struct mbuf; best of 5 on "
                    f"{threads} pinned threads; 1 thread: {gib / t1:.3f} GiB/s best of 3; "
                    f"results bit-identical to the GPU: {parity}"),
         "one_thread_gibs": round(gib / t1, 3),
@@ -261,7 +280,7 @@ def main():
                 "packets_per_gpu": n,
                 "algorithmic_bytes_per_gpu": w["bytes"],
                 "api": {"spans": "uinet_cksum_spans", "strided": "uinet_cksum_strided"}[args.api]
-                if args.config != "3" else "uinet_cksum_chains",
+                if args.config not in CHAIN_CONFIGS else "uinet_cksum_chains",
                 "parallelism": f"dp{world} packet shards" + (" + RCCL gather of u16 results"
                                                              if world > 1 else ""),
             },

@@ -14,6 +14,17 @@ config 3  1,048,576 packets of 64/576/1500 B (uniform), each chained into
 config 4  config 2's kernel per GPU, 2,097,152 packets per GPU (bench --packets).
 config 5  131,072 x 9000 B jumbo frames, in_cksum_pseudo_header(m, 8980, 20,
           src, dst, TCP/UDP): the pseudo-header seed per packet + 8980 bytes.
+
+Chain-shaped variants (uinet_cksum_chains), built by one layout function and
+materialised identically on the host (tests, oracle) or in HBM (bench):
+config 3tx  config 3's lengths in the reference TX shape: a header mbuf with
+          the 40-B IP+TCP header (tcp_output.c:844-846) chained to m_copy
+          slices of shuffled 4-KiB socket-buffer page clusters (:858); the
+          in_pseudo seed sits in th_sum (:1080-1081); in_cksum_skip(m, len, 20).
+config 5tso  TSO-style: 1-MiB sends cut at MSS 8960 (117 full segments + one
+          of 256 B); per segment a 40-B header chained to its payload slice of
+          the send buffer, in_cksum_pseudo_header(m, 20 + seglen, 20, src,
+          dst, TCP) -- the per-segment sums a TSO engine fills in.
 """
 from __future__ import annotations
 
@@ -171,3 +182,122 @@ def config5_device(n: int = 131072, frame: int = 9000, off0: int = 20, rank: int
     return dict(arena=arena, off=off, len=torch.full((n,), plen, dtype=torch.int32, device=device),
                 seed=torch.from_numpy(seed.view(np.int32)).to(device), n=n, bytes=n * plen,
                 src=src, dst=dst, proto=proto, plen=plen, off0=off0, frame=frame)
+
+
+# ---- chain-shaped variants ------------------------------------------------------
+
+def _bswap16(x):
+    x = np.asarray(x, np.uint64)
+    return ((x & np.uint64(0xFF)) << np.uint64(8)) | ((x >> np.uint64(8)) & np.uint64(0xFF))
+
+
+def _in_pseudo(a, b, c) -> np.ndarray:
+    s = np.asarray(a, np.uint64) + np.asarray(b, np.uint64) + np.asarray(c, np.uint64)
+    for _ in range(4):
+        s = (s & np.uint64(0xFFFF)) + (s >> np.uint64(16))
+    return s.astype(np.uint16)
+
+
+def _u16_patch(pos0, vals) -> tuple[np.ndarray, np.ndarray]:
+    """Byte positions/values that store the u16s `vals` (native LE) at pos0."""
+    v = np.asarray(vals, np.uint16)
+    pos = np.stack([pos0, pos0 + 1], 1).reshape(-1)
+    return pos.astype(np.int64), v.view(np.uint8).reshape(-1).copy()
+
+
+def config3tx_layout(n: int, seed: int = 33):
+    """Config 3's lengths in the reference TX chain shape (see module doc)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.choice(np.array([64, 576, 1500], np.int64), n)
+    pay = lens - 40
+    clus0 = 256 * n                      # header mbufs first, then page clusters
+    hdr_off = 256 * np.arange(n, dtype=np.int64) + 88 + 16   # pktdat + max_linkhdr
+    s0 = np.concatenate([[0], np.cumsum(pay)])[:-1]
+    total = int(pay.sum())
+    nclus = total // 4096 + 2
+    perm = rng.permutation(nclus).astype(np.int64)
+    c0, o0 = s0 // 4096, s0 % 4096
+    first = np.minimum(pay, 4096 - o0)
+    two = first < pay
+    nseg = 2 + two.astype(np.int64)
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)])
+    seg_off = np.zeros(int(pkt_seg[-1]), np.int64)
+    seg_len = np.zeros_like(seg_off)
+    h = pkt_seg[:-1]
+    seg_off[h], seg_len[h] = hdr_off, 40
+    seg_off[h + 1], seg_len[h + 1] = clus0 + perm[c0] * 4096 + o0, first
+    seg_off[h[two] + 2] = clus0 + perm[c0[two] + 1] * 4096
+    seg_len[h[two] + 2] = pay[two] - first[two]
+    src = rng.integers(0, 2**32, n, dtype=np.uint64)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64)
+    th = _in_pseudo(src, dst, _bswap16(6 + lens - 20))       # tcp_output.c:1080-1081
+    p1, v1 = _u16_patch(hdr_off + 36, th)
+    p2, v2 = _u16_patch(hdr_off + 10, np.zeros(n, np.uint16))  # ip_sum not yet set
+    return dict(n=n, lens=lens, skip=np.full(n, 20, np.int64), seed=None,
+                seg_off=seg_off, seg_len=seg_len, pkt_seg=pkt_seg,
+                patch_pos=np.concatenate([p1, p2]), patch_val=np.concatenate([v1, v2]),
+                arena_bytes=int(clus0 + nclus * 4096 + 64), stream_seed=SEED_BASE + 3 + 100,
+                bytes=int((lens - 20).sum()), hdr_off=hdr_off)
+
+
+def config5tso_layout(sends: int = 1111, mss: int = 8960, send_bytes: int = 1 << 20,
+                      seed: int = 55):
+    """TSO-style per-segment sums of 1-MiB sends (see module doc)."""
+    rng = np.random.default_rng(seed)
+    per = -(-send_bytes // mss)
+    seglen1 = np.full(per, mss, np.int64)
+    seglen1[-1] = send_bytes - mss * (per - 1)
+    n = sends * per
+    seglen = np.tile(seglen1, sends)
+    hdr_bytes = 64 * n
+    hdr_off = 64 * np.arange(n, dtype=np.int64)
+    pay_off = (hdr_bytes + send_bytes * np.repeat(np.arange(sends, dtype=np.int64), per)
+               + np.tile(mss * np.arange(per, dtype=np.int64), sends))
+    pkt_seg = 2 * np.arange(n + 1, dtype=np.int64)
+    seg_off = np.stack([hdr_off, pay_off], 1).reshape(-1)
+    seg_len = np.stack([np.full(n, 40, np.int64), seglen], 1).reshape(-1)
+    src = np.repeat(rng.integers(0, 2**32, sends, dtype=np.uint64), per)   # one flow per send
+    dst = np.repeat(rng.integers(0, 2**32, sends, dtype=np.uint64), per)
+    plen = 20 + seglen
+    p1, v1 = _u16_patch(hdr_off + 36, np.zeros(n, np.uint16))   # th_sum left to the engine
+    p2, v2 = _u16_patch(hdr_off + 10, np.zeros(n, np.uint16))
+    return dict(n=n, lens=40 + seglen, skip=np.full(n, 20, np.int64),
+                seed=pseudo_seed(src, dst, 6, plen), src=src, dst=dst, plen=plen, off0=20,
+                seg_off=seg_off, seg_len=seg_len, pkt_seg=pkt_seg,
+                patch_pos=np.concatenate([p1, p2]), patch_val=np.concatenate([v1, v2]),
+                arena_bytes=int(hdr_bytes + sends * send_bytes + 64),
+                stream_seed=SEED_BASE + 5 + 100, bytes=int(plen.sum()), sends=sends,
+                per_send=per, mss=mss)
+
+
+def chain_layout(cfg: str, n=None):
+    if cfg == "3tx":
+        return config3tx_layout(n or (1 << 20))
+    if cfg == "5tso":
+        return config5tso_layout(n or 1111)
+    raise ValueError(cfg)
+
+
+def materialize_host(lay) -> np.ndarray:
+    """The layout's arena in host memory (4-KiB aligned)."""
+    arena = aligned_empty(lay["arena_bytes"])
+    splitmix64_bytes(lay["arena_bytes"], lay["stream_seed"], out=arena)
+    arena[lay["patch_pos"]] = lay["patch_val"]
+    return arena
+
+
+def materialize_device(lay, device="cuda"):
+    """The same arena generated in HBM, plus the chain descriptors there."""
+    import torch
+
+    arena = torch.empty(lay["arena_bytes"], dtype=torch.uint8, device=device)
+    splitmix64_fill_device(arena, lay["stream_seed"])
+    arena[torch.from_numpy(lay["patch_pos"]).to(device)] = torch.from_numpy(lay["patch_val"]).to(device)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(device)  # noqa: E731
+    nseg = int(lay["seg_len"].size)
+    return dict(arena=arena, seg_off=t(lay["seg_off"], np.int64),
+                seg_len=t(lay["seg_len"], np.int32), pkt_seg=t(lay["pkt_seg"], np.int32),
+                len=t(lay["lens"], np.int32), skip=t(lay["skip"], np.int32),
+                seed=None if lay["seed"] is None else t(lay["seed"].view(np.int32), np.int32),
+                n=lay["n"], nseg=nseg, mean_seg=int(lay["seg_len"].sum() // max(1, nseg)),
+                bytes=lay["bytes"], layout=lay)

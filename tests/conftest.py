@@ -95,3 +95,15 @@ def gpu_available() -> bool:
         return torch.cuda.is_available()
     except Exception:  # pragma: no cover
         return False
+
+
+@pytest.fixture(scope="session")
+def torch_dev():
+    """torch on a visible gfx950 device (GPU tests only)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import libuinet_amd as u
+
+    assert u.device_ok(), "device is not gfx950"
+    return torch

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # One GPU-box session: parity tests, bench, rocprofv3 kernel trace + PMC pass.
 # Each GPU step has its own time limit; a fault/abort/timeout ends the script.
-# Usage: tools/gpu_session.sh <tag> [tests|bench|prof|host|all]
+# Usage: tools/gpu_session.sh <tag> [tests|bench|prof|host|variants|tests+host|tests+variants|all]
 set -u
 TAG=${1:-r01}
 WHAT=${2:-all}
@@ -20,7 +20,7 @@ run() { # name, seconds, command...
   if fatal $rc; then echo "FATAL step $name rc=$rc -- stopping"; exit $rc; fi
   return 0
 }
-if [[ $WHAT == all || $WHAT == tests || $WHAT == tests+host ]]; then
+if [[ $WHAT == all || $WHAT == tests || $WHAT == tests+host || $WHAT == tests+variants ]]; then
   run pytest_gpu 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider
 fi
 if [[ $WHAT == all || $WHAT == bench ]]; then
@@ -30,6 +30,12 @@ fi
 if [[ $WHAT == all || $WHAT == prof ]]; then
   run prof_trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline off
   run prof_pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats -d "$OUT/prof_pmc" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline off
+fi
+if [[ $WHAT == all || $WHAT == variants || $WHAT == tests+variants ]]; then
+  run bench_c3tx 600 python bench.py --steps 30 --warmup 5 --config 3tx
+  run bench_c5tso 600 python bench.py --steps 30 --warmup 5 --config 5tso
+  run prof_variants 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_variants" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --config 3tx --cpu-baseline off
+  run prof_variants_tso 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_variants_tso" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --config 5tso --cpu-baseline off
 fi
 if [[ $WHAT == all || $WHAT == host || $WHAT == tests+host ]]; then
   run echo_replay 600 python tools/echo_replay.py
