@@ -109,12 +109,15 @@ int uinet_cksum_device_ok(void);
  *   "blocks_per_cu"   grid-stride launch width, 0 = per-kernel default
  *   "chains_variant"  0 = flattened chunk stream (default), 1 = serial walk
  *   "chains_pass"     passes in flight per wave in the chain kernel: 2, 4, 8
+ *   "chains_long"     chain segments of at least this many 16-B chunks are
+ *                     streamed wave-wide; 0 = never, else >= 16 (default 128)
+ *   "chains_tile"     packets per wave in the chain kernel: 0 = auto, 8, 32
  *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
  *                     1..64 (default min(8, hardware threads))
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
- * (serial|flat), UINET_CKSUM_CHAINS_PASS and UINET_CKSUM_HOST_THREADS set the
- * initial values. */
+ * (serial|flat), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
+ * UINET_CKSUM_CHAINS_TILE and UINET_CKSUM_HOST_THREADS set the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
 /* ------------------------------------------------------------------------ */

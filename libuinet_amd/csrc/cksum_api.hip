@@ -62,7 +62,7 @@ int check_launch() { return record_hip(hipGetLastError()); }
 static Tuning& tuning_rw() {
   static Tuning t = [] {
     const unsigned hw = std::thread::hardware_concurrency();
-    Tuning x{0, 0, 2, (int)std::min(8u, hw ? hw : 1u)};
+    Tuning x{0, 0, 2, (int)std::min(8u, hw ? hw : 1u), 128, 0};
     if (const char* e = getenv("UINET_CKSUM_BLOCKS_PER_CU")) {
       const int v = atoi(e);
       x.blocks_per_cu = (v > 0 && v <= 4096) ? v : 0;
@@ -71,6 +71,14 @@ static Tuning& tuning_rw() {
     if (const char* e = getenv("UINET_CKSUM_CHAINS_PASS")) {
       const int v = atoi(e);
       if (v == 2 || v == 4 || v == 8) x.chains_pass = v;
+    }
+    if (const char* e = getenv("UINET_CKSUM_CHAINS_LONG")) {
+      const int v = atoi(e);
+      if (v == 0 || (v >= 16 && v <= (1 << 24))) x.chains_long = v;
+    }
+    if (const char* e = getenv("UINET_CKSUM_CHAINS_TILE")) {
+      const int v = atoi(e);
+      if (v == 0 || v == 8 || v == 32) x.chains_tile = v;
     }
     if (const char* e = getenv("UINET_CKSUM_HOST_THREADS")) {
       const int v = atoi(e);
@@ -567,6 +575,10 @@ int uinet_cksum_set_tuning(const char* key, int value) {
     t.chains_variant = value;
   } else if (!strcmp(key, "chains_pass") && (value == 2 || value == 4 || value == 8)) {
     t.chains_pass = value;
+  } else if (!strcmp(key, "chains_long") && (value == 0 || (value >= 16 && value <= (1 << 24)))) {
+    t.chains_long = value;
+  } else if (!strcmp(key, "chains_tile") && (value == 0 || value == 8 || value == 32)) {
+    t.chains_tile = value;
   } else if (!strcmp(key, "host_threads") && value >= 1 && value <= 64) {
     t.host_threads = value;
   } else {

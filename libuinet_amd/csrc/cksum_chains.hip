@@ -24,6 +24,11 @@
 //   * chunk sums are binned per packet with a plain DPP prefix sum P: the
 //     last lane of each run of equal slots adds +P to its slot and -P to the
 //     next run's slot (telescoping), into the wave's u64 LDS accumulators.
+//   * long segments (>= long_ch chunks) skip the chunk list: the whole wave
+//     streams each one like a span (no per-chunk segment lookup or binning)
+//     and adds one wave-reduced sum to its packet.
+// Tiles of 8 packets instead of 32 when the batch is small enough that 32
+// would leave too few waves to balance 256 CUs (e.g. jumbo frames).
 // k_chains (UINET_CKSUM_CHAINS=serial, kept for A/B) -- G lanes walk one
 // packet's segments one after another.
 #include <hip/hip_runtime.h>
@@ -72,10 +77,10 @@ __global__ __launch_bounds__(kBlock) void k_chains(const uint8_t* __restrict__ b
   }
 }
 
-constexpr int kTile = 32;              // packets per wave tile
 constexpr int kWaves = kBlock / 64;
+constexpr int kLongU = 4;  // chunks in flight per lane on a long segment
 
-template <int kPass>
+template <int kPass, int kTile>
 __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restrict__ base,
                                                        const uint64_t* __restrict__ seg_off,
                                                        const uint32_t* __restrict__ seg_len,
@@ -84,7 +89,8 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
                                                        const uint32_t* __restrict__ pskip,
                                                        const uint32_t* __restrict__ seed,
                                                        uint16_t* __restrict__ out, uint32_t n,
-                                                       uint32_t flags) {
+                                                       uint32_t flags, uint32_t long_ch) {
+  static_assert(kTile >= 1 && kTile <= 64, "a tile's packets are one per lane");
   constexpr int kWin = 64 * kPass;  // chunks per batch of passes
   __shared__ MaskLut lut;
   __shared__ unsigned long long lds_acc[kWaves][kTile];
@@ -153,14 +159,45 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
       const uint32_t rot = ((pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(base + ao)) & 1u;
       const uint32_t meta = (slot << 1) | rot;
       const uint32_t span = (eff << 4) | head;  // eff < 2^28
-      const uint32_t ci = wave_scan<0, false>(nch, 0u);
-      const uint32_t cst = ci - nch;  // first chunk of each segment in the round's list
-      const uint32_t C = __builtin_amdgcn_readlane(ci, 63);
       const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
+      // --- long segments: one wave-wide span each -------------------------
+      const bool is_long = long_ch != 0 && nch >= long_ch;
+      for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
+        const int s = (int)__builtin_ctzll(lm);
+        const uint32_t sp = __builtin_amdgcn_readlane(span, s);
+        const uint32_t mts = __builtin_amdgcn_readlane(meta, s);
+        const uint8_t* cb = base + (((uint64_t)__builtin_amdgcn_readlane(c0_hi, s) << 32) |
+                                    __builtin_amdgcn_readlane(c0_lo, s));
+        const int h = (int)(sp & 15), e = h + (int)(sp >> 4);
+        const uint32_t nc = __builtin_amdgcn_readlane(nch, s);
+        uint64_t lsum = 0;
+        for (uint32_t k0 = 0; k0 < nc; k0 += 64 * kLongU) {
+          // only the passes that hold chunks are issued (wave-uniform tests)
+          u32x4 v[kLongU];
+#pragma unroll
+          for (int u = 0; u < kLongU; ++u)
+            if (u == 0 || k0 + 64u * u < nc)
+              v[u] = load_chunk(cb + 16u * min(k0 + (uint32_t)(u * 64 + lane), nc - 1));
+#pragma unroll
+          for (int u = 0; u < kLongU; ++u) {
+            if (u == 0 || k0 + 64u * u < nc) {
+              const int b = 16 * (int)(k0 + (uint32_t)(u * 64 + lane));
+              lsum += lut.sum(v[u], h - b, e - b);  // chunks past the end: [h-b, e-b) empty
+            }
+          }
+        }
+        uint32_t x = fold16_32(__builtin_amdgcn_readlane(wave_scan<0, false>(fold16(lsum), 0u), 63));
+        if (mts & 1) x = rot8(x);
+        if (lane == 0) atomicAdd(&acc[mts >> 1], (unsigned long long)x);
+      }
+      const uint32_t nch_l = is_long ? 0u : nch;  // the chunk list holds the rest
+      const uint32_t ci = wave_scan<0, false>(nch_l, 0u);
+      const uint32_t cst = ci - nch_l;  // first chunk of each segment in the round's list
+      const uint32_t C = __builtin_amdgcn_readlane(ci, 63);
       // --- data: batches of kPass passes over the round's chunk list ------
       uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the pass
       for (uint32_t b = 0; b < C; b += kWin) {
-        const bool mk = nch != 0 && cst >= b && cst < b + kWin;
+        const bool mk = nch_l != 0 && cst >= b && cst < b + kWin;
         if (mk) mark[cst - b] = (uint8_t)(lane + 1);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         u32x4 v[kPass];
@@ -265,18 +302,27 @@ int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg
 #undef L
     return check_launch();
   }
-  const uint32_t tiles = (n + kTile - 1) / kTile;
+  // Tile of 32 packets, or 8 when 32 would give fewer than ~64 tiles per CU.
+  const int tile = tn.chains_tile ? tn.chains_tile : (n >= 32u * 16384u ? 32 : 8);
+  const uint32_t tiles = (n + (uint32_t)tile - 1) / (uint32_t)tile;
   uint64_t blocks = (tiles + kWaves - 1) / kWaves;
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
-#define LF(P)                                                                             \
-  hipLaunchKernelGGL((k_chains_flat<P>), dim3((int)blocks), dim3(kBlock), 0, stream, b,     \
-                     seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags)
-  switch (tn.chains_pass) {
-    case 2: LF(2); break;
-    case 8: LF(8); break;
-    case 4: LF(4); break;
-    default: LF(2); break;
+  const uint32_t long_ch = (uint32_t)tn.chains_long;
+#define LF(P, T)                                                                          \
+  hipLaunchKernelGGL((k_chains_flat<P, T>), dim3((int)blocks), dim3(kBlock), 0, stream, b,  \
+                     seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
+  if (tile == 8) {
+    switch (tn.chains_pass) {
+      case 4: LF(4, 8); break;
+      default: LF(2, 8); break;
+    }
+  } else {
+    switch (tn.chains_pass) {
+      case 8: LF(8, 32); break;
+      case 4: LF(4, 32); break;
+      default: LF(2, 32); break;
+    }
   }
 #undef LF
   return check_launch();

@@ -16,6 +16,9 @@ struct Tuning {
   int chains_variant;  // 0 flat, 1 serial
   int chains_pass;     // 2, 4, 8
   int host_threads;    // host-mbuf batch walk/pack threads, 1..64
+  int chains_long;     // flat chains: segments of >= this many 16-B chunks stream
+                       // wave-wide (0 = never)
+  int chains_tile;     // flat chains: packets per wave tile, 0 = auto, 8, 32
 };
 const Tuning& tuning();
 

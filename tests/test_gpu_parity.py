@@ -465,3 +465,39 @@ def test_host_batch_chunked(torch_dev, ora, host_threads):
             u.unregister_host(arena)
     finally:
         u.set_tuning("host_threads", 8)
+
+
+@pytest.mark.parametrize("long_ch,tile", [(0, 32), (16, 8), (16, 32), (64, 0), (200, 8)])
+def test_chains_long_segments(torch_dev, ora, long_ch, tile):
+    """Chains mixing short and long (wave-streamed) segments, with len/skip
+    clipping that cuts into long segments, over both tile sizes."""
+    torch = torch_dev
+    rng = np.random.default_rng(5100 + long_ch + tile)
+    arena = rand_arena(1 << 23, 51)
+    n = 3000
+    nseg = rng.integers(1, 7, n)
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = np.where(rng.random(s) < 0.5, rng.integers(0, 200, s), rng.integers(200, 9000, s))
+    seg_off = rng.integers(0, arena.size - 9100, s).astype(np.int64)
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1])
+    skip = np.where(rng.random(n) < 0.5, 20, (rng.random(n) * tot * 0.6).astype(np.int64))
+    length = np.where(rng.random(n) < 0.7, tot, skip + (rng.random(n) * (tot - skip + 1)).astype(np.int64))
+    seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
+    u.set_tuning("chains_long", long_ch)
+    u.set_tuning("chains_tile", tile)
+    try:
+        for flags in (0, u.F_UDP):
+            w = want if flags == 0 else ora.chains(arena, seg_off, seg_len, pkt_seg, length=length,
+                                                   skip=skip, seed=seed, flags=flags)
+            got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off),
+                                 dev(torch, seg_len.astype(np.int32)),
+                                 dev(torch, pkt_seg.astype(np.int32)),
+                                 length=dev(torch, length.astype(np.int32)),
+                                 skip=dev(torch, skip.astype(np.int32)),
+                                 seed=dev(torch, seed.view(np.int32)), flags=flags)
+            np.testing.assert_array_equal(host16(got), w)
+    finally:
+        u.set_tuning("chains_long", 128)
+        u.set_tuning("chains_tile", 0)
