@@ -36,9 +36,11 @@ extern "C" {
 #pragma GCC visibility push(default)
 #endif
 
-/* libuinet's struct mbuf (sys/sys/mbuf.h:153-171).  Only m_next (offset 0),
- * m_data (offset 16) and m_len (int, offset 24) are read; the chain is
- * borrowed read-only, never modified, freed or pulled up. */
+/* libuinet's struct mbuf (sys/sys/mbuf.h:153-171).  The checksum functions
+ * read only m_next (offset 0), m_data (offset 16) and m_len (int, offset 24);
+ * the chain is borrowed read-only, never modified, freed or pulled up.  Only
+ * the driver offload hooks (2d) write: m_pkthdr.csum_flags / csum_data
+ * (offsets 64 / 68) and, on TX, the checksum fields of the packet. */
 struct mbuf;
 /* struct ip (sys/netinet/ip.h:49-70): 20 bytes, ip_sum at offset 10. */
 struct ip;
@@ -182,6 +184,50 @@ int in_cksum_hdr_batch(const struct ip *const *ip, unsigned int *out, int n);
  * overlap; memory that is already pinned (hipHostMalloc) is accepted as is. */
 int uinet_cksum_register_host(void *base, size_t len);
 int uinet_cksum_unregister_host(void *base);
+
+/* ------------------------------------------------------------------------ */
+/* 2d. Driver batch offload            */
+/*                                                                          */
+/* Whole RX / TX batches of IPv4 packets, each one mbuf chain with          */
+/* M_PKTHDR set.  `l2len` is the byte offset of the IP header from m_data:  */
+/* -1 = parse an Ethernet header (14 bytes, 18 with one 802.1Q tag), 0 =    */
+/* m_data points at the IP header (ip_output's view).  One GPU batch per    */
+/* call; status[i] (may be NULL) receives UINET_RX_* / UINET_TX_* bits.     */
+/* ------------------------------------------------------------------------ */
+
+#define UINET_RX_IPV4    0x01 /* IPv4 header parsed */
+#define UINET_RX_IP_OK   0x02 /* header checksum verifies */
+#define UINET_RX_L4      0x04 /* TCP/UDP checksum computed */
+#define UINET_RX_L4_OK   0x08 /* ... and it verifies */
+#define UINET_RX_NOSUM   0x10 /* UDP datagram without checksum (uh_sum 0) */
+#define UINET_RX_FRAG    0x20 /* fragment: L4 left to the stack after reassembly */
+
+/* RX (first-look hook / uinet_pd_deliver_to_stack, uinet_api.c:2165-2187):
+ * verifies every packet's IPv4 header and TCP/UDP checksum and records the
+ * result in m_pkthdr the way a checksum-offloading NIC does, so ip_input
+ * (ip_input.c:460-471), tcp_input (tcp_input.c:697-718) and udp_input
+ * (udp_usrreq.c:428-449) skip the software sums yet reach the same verdict:
+ *   csum_flags |= CSUM_IP_CHECKED, | CSUM_IP_VALID when the header sums to 0;
+ *   TCP, and UDP with uh_sum != 0: csum_flags |= CSUM_DATA_VALID |
+ *   CSUM_PSEUDO_HDR, csum_data = in_cksum_pseudo_header(...) ^ 0xffff
+ *   (0xffff for a good packet, as if_loop.c:96-101 sets it).
+ * UDP covers uh_ulen bytes (udp_usrreq.c:404-412); fragments, truncated
+ * chains and non-IPv4 frames get no L4 marks. */
+int uinet_cksum_rx_offload(struct mbuf *const *m, int n, int l2len,
+    uint8_t *status);
+
+#define UINET_TX_L4      0x01 /* th_sum / uh_sum computed and stored */
+#define UINET_TX_IP      0x02 /* ip_sum computed and stored */
+#define UINET_TX_L4_LOST 0x04 /* checksum field beyond the first mbuf: not stored */
+#define UINET_TX_SKIP    0x08 /* no M_PKTHDR, not IPv4, or CSUM_TSO */
+
+/* TX (if_netmap_batch_send, uinet_if_netmap.c:1196-1262, with if_hwassist =
+ * CSUM_IP|CSUM_TCP|CSUM_UDP so ip_output defers, ip_output.c:645-656): for
+ * every packet whose csum_flags ask for it, does what in_delayed_cksum
+ * (ip_output.c:953-976, the in_pseudo seed already in th_sum) and the
+ * ip_sum store (:665-667) do, then clears those csum_flags bits. */
+int uinet_cksum_tx_offload(struct mbuf *const *m, int n, int l2len,
+    uint8_t *status);
 
 #if defined(__GNUC__)
 #pragma GCC visibility pop

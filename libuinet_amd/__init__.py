@@ -48,7 +48,12 @@ EXPORTED_SYMBOLS = (
     "uinet_cksum_device_ok", "uinet_cksum_set_tuning", "uinet_cksum_spans", "uinet_cksum_strided", "uinet_cksum_chains",
     "in_cksum_skip_batch", "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch",
     "uinet_cksum_register_host", "uinet_cksum_unregister_host",
+    "uinet_cksum_rx_offload", "uinet_cksum_tx_offload",
 )
+
+# Driver offload status bits (include/uinet_cksum.h section 2d).
+RX_IPV4, RX_IP_OK, RX_L4, RX_L4_OK, RX_NOSUM, RX_FRAG = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
+TX_L4, TX_IP, TX_L4_LOST, TX_SKIP = 0x01, 0x02, 0x04, 0x08
 
 
 class CksumError(RuntimeError):
@@ -100,6 +105,8 @@ def lib() -> ctypes.CDLL:
         "in_cksum_hdr_batch": (_i32, [_vp, _vp, _i32]),
         "uinet_cksum_register_host": (_i32, [_vp, ctypes.c_size_t]),
         "uinet_cksum_unregister_host": (_i32, [_vp]),
+        "uinet_cksum_rx_offload": (_i32, [_vp, _i32, _i32, _vp]),
+        "uinet_cksum_tx_offload": (_i32, [_vp, _i32, _i32, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -185,6 +192,26 @@ def register_host(buf: np.ndarray) -> None:
 
 def unregister_host(buf: np.ndarray) -> None:
     _check("uinet_cksum_unregister_host", lib().uinet_cksum_unregister_host(buf.ctypes.data))
+
+
+def rx_offload(heads, l2len: int = -1) -> np.ndarray:
+    """uinet_cksum_rx_offload: verify a received batch and mark m_pkthdr
+    (csum_flags / csum_data) like a checksum-offloading NIC; RX_* bits."""
+    heads = np.ascontiguousarray(heads, dtype=np.uint64)
+    st = np.zeros(heads.size, dtype=np.uint8)
+    _check("uinet_cksum_rx_offload",
+           lib().uinet_cksum_rx_offload(_ptr(heads), heads.size, l2len, _ptr(st)))
+    return st
+
+
+def tx_offload(heads, l2len: int = -1) -> np.ndarray:
+    """uinet_cksum_tx_offload: fill the deferred ip_sum / th_sum / uh_sum of a
+    transmit batch in place (in_delayed_cksum semantics); TX_* bits."""
+    heads = np.ascontiguousarray(heads, dtype=np.uint64)
+    st = np.zeros(heads.size, dtype=np.uint8)
+    _check("uinet_cksum_tx_offload",
+           lib().uinet_cksum_tx_offload(_ptr(heads), heads.size, l2len, _ptr(st)))
+    return st
 
 
 def in_cksum_hdr_batch(ips) -> np.ndarray:

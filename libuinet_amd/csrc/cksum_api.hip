@@ -31,21 +31,10 @@
 #include <vector>
 
 #include "cksum_internal.h"
+#include "host_batch.h"
 #include "host_pool.h"
 
 namespace uinet {
-
-// The three fields of struct m_hdr the checksum reads
-// (sys/sys/mbuf.h:90-98): m_next@0, m_data@16, m_len@24.
-struct MbufHdr {
-  MbufHdr* m_next;
-  void* m_nextpkt;
-  const uint8_t* m_data;
-  int m_len;
-};
-static_assert(offsetof(MbufHdr, m_next) == 0, "m_next offset");
-static_assert(offsetof(MbufHdr, m_data) == 16, "m_data offset");
-static_assert(offsetof(MbufHdr, m_len) == 24, "m_len offset");
 
 static thread_local int t_last_hip = 0;
 
@@ -497,6 +486,18 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   }
   return UINET_CKSUM_OK;
 }
+
+}  // namespace
+
+int run_jobs(const Job* jobs, int n, uint16_t* out) {
+  if (n > 0 && (!jobs || !out)) return UINET_CKSUM_EINVAL;
+  return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
+    w.walk_skip(jobs[i].m, jobs[i].len, jobs[i].skip);
+    return jobs[i].seed;
+  });
+}
+
+namespace {
 
 [[noreturn]] void die(const char* fn, int rc) {
   fprintf(stderr, "libuinet_cksum: %s failed: %s (hip error %d: %s)\n", fn,

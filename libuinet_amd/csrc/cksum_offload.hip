@@ -1,0 +1,270 @@
+// Driver batch offload: whole RX / TX batches of
+// IPv4 packets checksummed in one GPU batch, with the results recorded the
+// way the stack consumes a checksum-offloading NIC's work.
+//
+//   RX  ip_input.c:460-471 (CSUM_IP_CHECKED / CSUM_IP_VALID),
+//       tcp_input.c:697-718 and udp_usrreq.c:428-449 (CSUM_DATA_VALID |
+//       CSUM_PSEUDO_HDR: th_sum = csum_data ^ 0xffff must be 0).
+//   TX  ip_output.c:645-667 (deferred ip_sum) and :953-976 (in_delayed_cksum:
+//       in_cksum_skip(m, ip_len, hlen) over the in_pseudo seed already in
+//       th_sum, UDP 0 -> 0xffff, stored at hlen + csum_data).
+//
+// The host parses headers (a few bytes per packet, already in cache from the
+// driver) and writes flags; every byte sum is a GPU job (host_batch.h).
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "cksum_internal.h"
+#include "host_batch.h"
+
+namespace uinet {
+namespace {
+
+// sys/sys/mbuf.h:182,281-293; sys/netinet/ip.h:63-65.
+constexpr int kMPktHdr = 0x2;
+constexpr int kCsumIp = 0x1, kCsumTcp = 0x2, kCsumUdp = 0x4, kCsumTso = 0x20;
+constexpr int kCsumIpChecked = 0x100, kCsumIpValid = 0x200, kCsumDataValid = 0x400,
+              kCsumPseudoHdr = 0x800;
+constexpr int kIpMf = 0x2000, kIpOffMask = 0x1fff;
+
+// Copies up to n bytes at chain offset `off`; returns the count copied.
+int chain_read(const MbufHdr* m, int off, uint8_t* dst, int n) {
+  int got = 0;
+  for (; m && got < n; m = m->m_next) {
+    const int l = m->m_len;
+    if (l <= 0) continue;
+    if (off >= l) {
+      off -= l;
+      continue;
+    }
+    const int k = (l - off < n - got) ? l - off : n - got;
+    memcpy(dst + got, m->m_data + off, (size_t)k);
+    got += k;
+    off = 0;
+  }
+  return got;
+}
+
+long chain_len(const MbufHdr* m) {
+  long t = 0;
+  for (; m; m = m->m_next) t += m->m_len > 0 ? m->m_len : 0;
+  return t;
+}
+
+inline uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+inline uint16_t bswap16(uint16_t x) { return (uint16_t)((x << 8) | (x >> 8)); }
+
+struct Ip4 {
+  int l3 = 0;       // chain offset of the IP header
+  int hl = 0;       // header length
+  int ip_len = 0;   // total length
+  int proto = 0;
+  bool frag = false;
+  uint32_t src = 0, dst = 0;  // as stored (network order read as a native u32)
+  uint8_t l4[8] = {};         // first 8 bytes after the IP header (if present)
+  int l4_have = 0;
+};
+
+// l2len -1: Ethernet (0x0800, or one 802.1Q tag then 0x0800).
+bool parse_ip4(const MbufHdr* m, int l2len, Ip4* o) {
+  uint8_t b[18 + 60 + 8];
+  int l3 = l2len;
+  if (l2len < 0) {
+    const int got = chain_read(m, 0, b, 18);
+    if (got < 14) return false;
+    uint16_t et = be16(b + 12);
+    l3 = 14;
+    if (et == 0x8100) {
+      if (got < 18) return false;
+      et = be16(b + 16);
+      l3 = 18;
+    }
+    if (et != 0x0800) return false;
+  }
+  const int got = chain_read(m, l3, b, 60 + 8);
+  if (got < 20 || (b[0] >> 4) != 4) return false;
+  const int hl = (b[0] & 15) * 4;
+  if (hl < 20 || got < hl) return false;
+  o->l3 = l3;
+  o->hl = hl;
+  o->ip_len = be16(b + 2);
+  o->frag = (be16(b + 6) & (kIpMf | kIpOffMask)) != 0;
+  o->proto = b[9];
+  memcpy(&o->src, b + 12, 4);
+  memcpy(&o->dst, b + 16, 4);
+  o->l4_have = got - hl < 8 ? got - hl : 8;
+  memcpy(o->l4, b + hl, (size_t)o->l4_have);
+  return true;
+}
+
+uint32_t fold16(uint64_t s) {
+  while (s >> 16) s = (s & 0xffff) + (s >> 16);
+  return (uint32_t)s;
+}
+
+// in_cksum.c:252-253, folded so it fits a job seed.
+uint32_t pseudo_seed(uint32_t src, uint32_t dst, int proto, int plen) {
+  return fold16((uint64_t)src + dst + bswap16((uint16_t)proto) + bswap16((uint16_t)plen));
+}
+
+struct RxPlan {
+  Ip4 ip;
+  int ip_job = -1, l4_job = -1;
+  uint8_t st = 0;
+};
+
+struct TxPlan {
+  Ip4 ip;
+  int ip_job = -1, l4_job = -1;
+  int l4_store = 0;  // chain offset of th_sum / uh_sum
+  bool udp = false;
+  uint8_t st = 0;
+};
+
+thread_local std::vector<Job> t_jobs;
+thread_local std::vector<uint16_t> t_res;
+thread_local std::vector<RxPlan> t_rx;
+thread_local std::vector<TxPlan> t_tx;
+
+}  // namespace
+}  // namespace uinet
+
+using namespace uinet;
+
+extern "C" {
+
+int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
+  if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
+  std::vector<Job>& jobs = t_jobs;
+  std::vector<RxPlan>& plan = t_rx;
+  jobs.clear();
+  plan.assign((size_t)n, RxPlan());
+  for (int i = 0; i < n; i++) {
+    const MbufHdr* m = reinterpret_cast<const MbufHdr*>(mv[i]);
+    RxPlan& p = plan[(size_t)i];
+    if (!m || !parse_ip4(m, l2len, &p.ip)) continue;
+    const Ip4& ip = p.ip;
+    p.st |= UINET_RX_IPV4;
+    p.ip_job = (int)jobs.size();  // in_cksum(m, hlen) over the header (ip_input.c:463-467)
+    jobs.push_back({m, ip.l3 + ip.hl, ip.l3, 0u});
+    if (ip.frag) {
+      p.st |= UINET_RX_FRAG;
+      continue;
+    }
+    if (ip.ip_len < ip.hl || chain_len(m) < (long)ip.l3 + ip.ip_len) continue;
+    int plen = ip.ip_len - ip.hl;
+    if (ip.proto == 6) {  // tcp_input.c:711-713: tlen = ip_len - off0
+    } else if (ip.proto == 17) {
+      if (ip.l4_have < 8) continue;
+      if (be16(ip.l4 + 6) == 0) {  // uh_sum 0: no checksum (udp_usrreq.c:427,450)
+        p.st |= UINET_RX_NOSUM;
+        continue;
+      }
+      const int ulen = be16(ip.l4 + 4);  // udp_usrreq.c:404-412
+      if (ulen > plen || ulen < 8) continue;
+      plen = ulen;
+    } else {
+      continue;
+    }
+    p.l4_job = (int)jobs.size();
+    jobs.push_back({m, ip.l3 + ip.hl + plen, ip.l3 + ip.hl,
+                    pseudo_seed(ip.src, ip.dst, ip.proto, plen)});
+  }
+  std::vector<uint16_t>& res = t_res;
+  res.resize(jobs.size());
+  const int rc = run_jobs(jobs.data(), (int)jobs.size(), res.data());
+  if (rc) return rc;
+  for (int i = 0; i < n; i++) {
+    RxPlan& p = plan[(size_t)i];
+    MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
+    const bool hdr = m && (m->m_flags & kMPktHdr);
+    if (p.ip_job >= 0) {
+      const bool ok = res[(size_t)p.ip_job] == 0;
+      p.st |= ok ? UINET_RX_IP_OK : 0;
+      if (hdr) pkthdr_of(m)->csum_flags |= kCsumIpChecked | (ok ? kCsumIpValid : 0);
+    }
+    if (p.l4_job >= 0) {
+      const uint16_t r = res[(size_t)p.l4_job];
+      p.st |= UINET_RX_L4 | (r == 0 ? UINET_RX_L4_OK : 0);
+      if (hdr) {
+        PktHdr* ph = pkthdr_of(m);
+        ph->csum_flags |= kCsumDataValid | kCsumPseudoHdr;
+        ph->csum_data = r ^ 0xffff;
+      }
+    }
+    if (status) status[i] = p.st;
+  }
+  return UINET_CKSUM_OK;
+}
+
+int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
+  if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
+  std::vector<Job>& jobs = t_jobs;
+  std::vector<TxPlan>& plan = t_tx;
+  jobs.clear();
+  plan.assign((size_t)n, TxPlan());
+  for (int i = 0; i < n; i++) {
+    MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
+    TxPlan& p = plan[(size_t)i];
+    if (!m || !(m->m_flags & kMPktHdr)) {
+      p.st = UINET_TX_SKIP;
+      continue;
+    }
+    const int fl = pkthdr_of(m)->csum_flags;
+    if ((fl & kCsumTso) || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) ||
+        !parse_ip4(m, l2len, &p.ip)) {
+      p.st = UINET_TX_SKIP;
+      continue;
+    }
+    const Ip4& ip = p.ip;
+    if (fl & (kCsumTcp | kCsumUdp)) {  // in_delayed_cksum, ip_output.c:958-963
+      p.udp = (fl & kCsumUdp) != 0;
+      p.l4_store = ip.l3 + ip.hl + pkthdr_of(m)->csum_data;
+      p.l4_job = (int)jobs.size();
+      jobs.push_back({m, ip.l3 + ip.ip_len, ip.l3 + ip.hl, 0u});
+    }
+    if (fl & kCsumIp) {  // ip_output.c:665-667: ip_sum = 0, then in_cksum(m, hlen)
+      if (ip.l3 + 12 > m->m_len) {
+        p.st = UINET_TX_SKIP;  // header not in the first mbuf: leave it to the stack
+        if (p.l4_job >= 0) jobs.pop_back();
+        p.l4_job = -1;
+        continue;
+      }
+      m->m_data[ip.l3 + 10] = 0;
+      m->m_data[ip.l3 + 11] = 0;
+      p.ip_job = (int)jobs.size();
+      jobs.push_back({m, ip.l3 + ip.hl, ip.l3, 0u});
+    }
+  }
+  std::vector<uint16_t>& res = t_res;
+  res.resize(jobs.size());
+  const int rc = run_jobs(jobs.data(), (int)jobs.size(), res.data());
+  if (rc) return rc;
+  for (int i = 0; i < n; i++) {
+    TxPlan& p = plan[(size_t)i];
+    MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
+    if (p.l4_job >= 0) {
+      uint16_t c = res[(size_t)p.l4_job];
+      if (p.udp && c == 0) c = 0xffff;  // ip_output.c:962-963
+      if (p.l4_store + 2 > m->m_len) {
+        p.st |= UINET_TX_L4_LOST;  // ip_output.c:966-974: the reference gives up too
+      } else {
+        memcpy(m->m_data + p.l4_store, &c, 2);
+        p.st |= UINET_TX_L4;
+      }
+      pkthdr_of(m)->csum_flags &= ~(kCsumTcp | kCsumUdp);
+    }
+    if (p.ip_job >= 0) {
+      const uint16_t c = res[(size_t)p.ip_job];
+      memcpy(m->m_data + p.ip.l3 + 10, &c, 2);
+      p.st |= UINET_TX_IP;
+      pkthdr_of(m)->csum_flags &= ~kCsumIp;
+    }
+    if (status) status[i] = p.st;
+  }
+  return UINET_CKSUM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// Host-side mbuf view and the walked-batch entry point shared by the C ABI
+// (cksum_api.hip) and the driver offload hooks (cksum_offload.hip).
+// Internal; not part of the C ABI.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+namespace uinet {
+
+// struct m_hdr (sys/sys/mbuf.h:90-98) on amd64: M_HDR_PAD 6 (:82), 40 bytes.
+struct MbufHdr {
+  MbufHdr* m_next;
+  void* m_nextpkt;
+  uint8_t* m_data;
+  int m_len;
+  int m_flags;
+  short m_type;
+  uint8_t pad[6];
+};
+static_assert(offsetof(MbufHdr, m_next) == 0, "m_next offset");
+static_assert(offsetof(MbufHdr, m_data) == 16, "m_data offset");
+static_assert(offsetof(MbufHdr, m_len) == 24, "m_len offset");
+static_assert(offsetof(MbufHdr, m_flags) == 28, "m_flags offset");
+static_assert(sizeof(MbufHdr) == 40, "struct m_hdr size");
+
+// struct pkthdr (sys/sys/mbuf.h:116-133), right after m_hdr when M_PKTHDR.
+struct PktHdr {
+  void* rcvif;
+  void* header;
+  int len;
+  uint32_t flowid;
+  int csum_flags;
+  int csum_data;
+  uint16_t tso_segsz;
+  uint16_t vtag;
+  void* tags;
+};
+static_assert(offsetof(PktHdr, csum_flags) == 24, "csum_flags at mbuf+64");
+static_assert(offsetof(PktHdr, csum_data) == 28, "csum_data at mbuf+68");
+static_assert(sizeof(MbufHdr) + sizeof(PktHdr) == 88, "m_pktdat at mbuf+88 (MHLEN 168)");
+
+inline PktHdr* pkthdr_of(MbufHdr* m) {
+  return reinterpret_cast<PktHdr*>(reinterpret_cast<uint8_t*>(m) + sizeof(MbufHdr));
+}
+
+// One in_cksum_skip(m, len, skip) with `seed` added to the sum before the
+// complement (0 for plain in_cksum_skip).
+struct Job {
+  const MbufHdr* m;
+  int len;
+  int skip;
+  uint32_t seed;
+};
+
+// Folds every job on the GPU in one batch (walk, zero-copy or staging, one
+// launch).  Returns a UINET_CKSUM_* code.
+int run_jobs(const Job* jobs, int n, uint16_t* out);
+
+}  // namespace uinet

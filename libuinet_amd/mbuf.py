@@ -17,6 +17,10 @@ from __future__ import annotations
 import numpy as np
 
 MSIZE = 256
+M_PKTHDR = 0x2  # sys/sys/mbuf.h:182
+# struct m_hdr (mbuf.h:90-98, M_HDR_PAD 6 on amd64) then struct pkthdr
+# (:116-133), valid in the first mbuf of a packet (M_PKTHDR); the driver
+# offload hooks read/write csum_flags and csum_data.
 MBUF_DTYPE = np.dtype(
     [
         ("m_next", "<u8"),
@@ -25,11 +29,24 @@ MBUF_DTYPE = np.dtype(
         ("m_len", "<i4"),
         ("m_flags", "<i4"),
         ("m_type", "<i2"),
-        ("m_pad", "V222"),
+        ("m_pad", "V6"),
+        ("rcvif", "<u8"),
+        ("header", "<u8"),
+        ("pkt_len", "<i4"),
+        ("flowid", "<u4"),
+        ("csum_flags", "<i4"),
+        ("csum_data", "<i4"),
+        ("tso_segsz", "<u2"),
+        ("vtag", "<u2"),
+        ("ph_pad", "V4"),
+        ("tags", "<u8"),
+        ("m_pktdat", "V168"),
     ]
 )
 assert MBUF_DTYPE.itemsize == MSIZE
 assert MBUF_DTYPE.fields["m_data"][1] == 16 and MBUF_DTYPE.fields["m_len"][1] == 24
+assert MBUF_DTYPE.fields["csum_flags"][1] == 64 and MBUF_DTYPE.fields["csum_data"][1] == 68
+assert MBUF_DTYPE.fields["m_pktdat"][1] == 88
 
 
 def aligned_empty(nbytes: int, align: int = 4096, pad: int = 64) -> np.ndarray:
@@ -73,6 +90,9 @@ class MbufChains:
         heads = np.zeros(npk, dtype=np.uint64)
         if nseg:
             heads[nonempty] = addr[pkt_seg[:-1][nonempty]]
+            first = pkt_seg[:-1][nonempty]
+            self.mbufs["m_flags"][first] = M_PKTHDR
+            self.mbufs["pkt_len"][first] = np.add.reduceat(seg_len, first) if first.size else 0
         self.heads = heads
 
     @property
@@ -81,6 +101,10 @@ class MbufChains:
 
     def head(self, i: int) -> int:
         return int(self.heads[i])
+
+    def first_mbuf(self, i: int) -> int:
+        """Index into ``mbufs`` of packet ``i``'s head (its pkthdr)."""
+        return int(self.pkt_seg[i])
 
     def packet_bytes(self, i: int) -> bytes:
         """The concatenated bytes of packet ``i``'s chain (test helper)."""

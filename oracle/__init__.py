@@ -60,6 +60,8 @@ class Oracle:
             "oracle_cksum_skip_batch": (None, [_vp, _vp, _vp, _vp, _i32, _i32]),
             "oracle_cksum_pseudo_header_batch": (None, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32]),
             "oracle_cksum_hdr_batch": (None, [_vp, _vp, _i32]),
+            "oracle_rx_offload": (None, [_vp, _i32, _i32, _vp]),
+            "oracle_tx_offload": (None, [_vp, _i32, _i32, _vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -106,6 +108,20 @@ class Oracle:
         out = np.zeros(ips.size, np.uint32)
         self.L.oracle_cksum_hdr_batch(_p(ips), _p(out), ips.size)
         return out
+
+    def rx_offload(self, heads, l2len: int = -1) -> np.ndarray:
+        """offload_oracle.c: the RX hook restated packet by packet (marks pkthdrs)."""
+        heads = _c(heads, np.uint64)
+        st = np.zeros(heads.size, np.uint8)
+        self.L.oracle_rx_offload(_p(heads), heads.size, l2len, _p(st))
+        return st
+
+    def tx_offload(self, heads, l2len: int = -1) -> np.ndarray:
+        """offload_oracle.c: the TX hook restated (writes sums into the packets)."""
+        heads = _c(heads, np.uint64)
+        st = np.zeros(heads.size, np.uint8)
+        self.L.oracle_tx_offload(_p(heads), heads.size, l2len, _p(st))
+        return st
 
     def spans(self, base: np.ndarray, off, length, seed=None, parity=None, flags=0) -> np.ndarray:
         off = _c(off, np.uint64)

@@ -43,4 +43,11 @@ void oracle_cksum_pseudo_header_batch(struct oracle_mbuf *const *m,
     const uint32_t *dst, const uint8_t *proto, uint16_t *out, int n);
 void oracle_cksum_hdr_batch(const void *const *ip, unsigned *out, int n);
 
+/* offload_oracle.c: the driver batch offload hooks, restated packet by
+ * packet (mutates pkthdr csum fields, and packet bytes on TX). */
+void oracle_rx_offload(struct oracle_mbuf *const *m, int n, int l2len,
+    uint8_t *status);
+void oracle_tx_offload(struct oracle_mbuf *const *m, int n, int l2len,
+    uint8_t *status);
+
 #endif
