@@ -18,6 +18,7 @@
 
 #include "cksum_internal.h"
 #include "host_batch.h"
+#include "host_pool.h"
 
 namespace uinet {
 namespace {
@@ -109,15 +110,17 @@ uint32_t pseudo_seed(uint32_t src, uint32_t dst, int proto, int plen) {
   return fold16((uint64_t)src + dst + bswap16((uint16_t)proto) + bswap16((uint16_t)plen));
 }
 
+// Packet i owns jobs 2i (IP header) and 2i+1 (TCP/UDP); an unused job has
+// m == nullptr and walks nothing.
 struct RxPlan {
   Ip4 ip;
-  int ip_job = -1, l4_job = -1;
+  bool ip_job = false, l4_job = false;
   uint8_t st = 0;
 };
 
 struct TxPlan {
   Ip4 ip;
-  int ip_job = -1, l4_job = -1;
+  bool ip_job = false, l4_job = false;
   int l4_store = 0;  // chain offset of th_sum / uh_sum
   bool udp = false;
   uint8_t st = 0;
@@ -128,6 +131,16 @@ thread_local std::vector<uint16_t> t_res;
 thread_local std::vector<RxPlan> t_rx;
 thread_local std::vector<TxPlan> t_tx;
 
+// f(i0, i1) over chunks of consecutive packets, on the host pool.
+template <typename F>
+void for_chunks(int n, F&& f) {
+  const int threads = tuning().host_threads;
+  int cs = (n + threads * 4 - 1) / (threads * 4);
+  if (cs < 1024) cs = 1024;
+  const int nch = (n + cs - 1) / cs;
+  host_pool().run(nch, threads, [&](int j) { f(j * cs, j * cs + cs < n ? j * cs + cs : n); });
+}
+
 }  // namespace
 }  // namespace uinet
 
@@ -137,133 +150,141 @@ extern "C" {
 
 int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
   if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
+  if (n == 0) return UINET_CKSUM_OK;
   std::vector<Job>& jobs = t_jobs;
   std::vector<RxPlan>& plan = t_rx;
-  jobs.clear();
+  jobs.assign(2 * (size_t)n, Job{nullptr, 0, 0, 0u});
   plan.assign((size_t)n, RxPlan());
-  for (int i = 0; i < n; i++) {
-    const MbufHdr* m = reinterpret_cast<const MbufHdr*>(mv[i]);
-    RxPlan& p = plan[(size_t)i];
-    if (!m || !parse_ip4(m, l2len, &p.ip)) continue;
-    const Ip4& ip = p.ip;
-    p.st |= UINET_RX_IPV4;
-    p.ip_job = (int)jobs.size();  // in_cksum(m, hlen) over the header (ip_input.c:463-467)
-    jobs.push_back({m, ip.l3 + ip.hl, ip.l3, 0u});
-    if (ip.frag) {
-      p.st |= UINET_RX_FRAG;
-      continue;
-    }
-    if (ip.ip_len < ip.hl || chain_len(m) < (long)ip.l3 + ip.ip_len) continue;
-    int plen = ip.ip_len - ip.hl;
-    if (ip.proto == 6) {  // tcp_input.c:711-713: tlen = ip_len - off0
-    } else if (ip.proto == 17) {
-      if (ip.l4_have < 8) continue;
-      if (be16(ip.l4 + 6) == 0) {  // uh_sum 0: no checksum (udp_usrreq.c:427,450)
-        p.st |= UINET_RX_NOSUM;
+  for_chunks(n, [&](int i0, int i1) {
+    for (int i = i0; i < i1; i++) {
+      const MbufHdr* m = reinterpret_cast<const MbufHdr*>(mv[i]);
+      RxPlan& p = plan[(size_t)i];
+      if (!m || !parse_ip4(m, l2len, &p.ip)) continue;
+      const Ip4& ip = p.ip;
+      p.st |= UINET_RX_IPV4;
+      p.ip_job = true;  // in_cksum(m, hlen) over the header (ip_input.c:463-467)
+      jobs[2 * (size_t)i] = {m, ip.l3 + ip.hl, ip.l3, 0u};
+      if (ip.frag) {
+        p.st |= UINET_RX_FRAG;
         continue;
       }
-      const int ulen = be16(ip.l4 + 4);  // udp_usrreq.c:404-412
-      if (ulen > plen || ulen < 8) continue;
-      plen = ulen;
-    } else {
-      continue;
+      if (ip.ip_len < ip.hl || chain_len(m) < (long)ip.l3 + ip.ip_len) continue;
+      int plen = ip.ip_len - ip.hl;
+      if (ip.proto == 6) {  // tcp_input.c:711-713: tlen = ip_len - off0
+      } else if (ip.proto == 17) {
+        if (ip.l4_have < 8) continue;
+        if (be16(ip.l4 + 6) == 0) {  // uh_sum 0: no checksum (udp_usrreq.c:427,450)
+          p.st |= UINET_RX_NOSUM;
+          continue;
+        }
+        const int ulen = be16(ip.l4 + 4);  // udp_usrreq.c:404-412
+        if (ulen > plen || ulen < 8) continue;
+        plen = ulen;
+      } else {
+        continue;
+      }
+      p.l4_job = true;
+      jobs[2 * (size_t)i + 1] = {m, ip.l3 + ip.hl + plen, ip.l3 + ip.hl,
+                                 pseudo_seed(ip.src, ip.dst, ip.proto, plen)};
     }
-    p.l4_job = (int)jobs.size();
-    jobs.push_back({m, ip.l3 + ip.hl + plen, ip.l3 + ip.hl,
-                    pseudo_seed(ip.src, ip.dst, ip.proto, plen)});
-  }
+  });
   std::vector<uint16_t>& res = t_res;
   res.resize(jobs.size());
   const int rc = run_jobs(jobs.data(), (int)jobs.size(), res.data());
   if (rc) return rc;
-  for (int i = 0; i < n; i++) {
-    RxPlan& p = plan[(size_t)i];
-    MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
-    const bool hdr = m && (m->m_flags & kMPktHdr);
-    if (p.ip_job >= 0) {
-      const bool ok = res[(size_t)p.ip_job] == 0;
-      p.st |= ok ? UINET_RX_IP_OK : 0;
-      if (hdr) pkthdr_of(m)->csum_flags |= kCsumIpChecked | (ok ? kCsumIpValid : 0);
-    }
-    if (p.l4_job >= 0) {
-      const uint16_t r = res[(size_t)p.l4_job];
-      p.st |= UINET_RX_L4 | (r == 0 ? UINET_RX_L4_OK : 0);
-      if (hdr) {
-        PktHdr* ph = pkthdr_of(m);
-        ph->csum_flags |= kCsumDataValid | kCsumPseudoHdr;
-        ph->csum_data = r ^ 0xffff;
+  for_chunks(n, [&](int i0, int i1) {
+    for (int i = i0; i < i1; i++) {
+      RxPlan& p = plan[(size_t)i];
+      MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
+      const bool hdr = m && (m->m_flags & kMPktHdr);
+      if (p.ip_job) {
+        const bool ok = res[2 * (size_t)i] == 0;
+        p.st |= ok ? UINET_RX_IP_OK : 0;
+        if (hdr) pkthdr_of(m)->csum_flags |= kCsumIpChecked | (ok ? kCsumIpValid : 0);
       }
+      if (p.l4_job) {
+        const uint16_t r = res[2 * (size_t)i + 1];
+        p.st |= UINET_RX_L4 | (r == 0 ? UINET_RX_L4_OK : 0);
+        if (hdr) {
+          PktHdr* ph = pkthdr_of(m);
+          ph->csum_flags |= kCsumDataValid | kCsumPseudoHdr;
+          ph->csum_data = r ^ 0xffff;
+        }
+      }
+      if (status) status[i] = p.st;
     }
-    if (status) status[i] = p.st;
-  }
+  });
   return UINET_CKSUM_OK;
 }
 
 int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
   if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
+  if (n == 0) return UINET_CKSUM_OK;
   std::vector<Job>& jobs = t_jobs;
   std::vector<TxPlan>& plan = t_tx;
-  jobs.clear();
+  jobs.assign(2 * (size_t)n, Job{nullptr, 0, 0, 0u});
   plan.assign((size_t)n, TxPlan());
-  for (int i = 0; i < n; i++) {
-    MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
-    TxPlan& p = plan[(size_t)i];
-    if (!m || !(m->m_flags & kMPktHdr)) {
-      p.st = UINET_TX_SKIP;
-      continue;
-    }
-    const int fl = pkthdr_of(m)->csum_flags;
-    if ((fl & kCsumTso) || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) ||
-        !parse_ip4(m, l2len, &p.ip)) {
-      p.st = UINET_TX_SKIP;
-      continue;
-    }
-    const Ip4& ip = p.ip;
-    if (fl & (kCsumTcp | kCsumUdp)) {  // in_delayed_cksum, ip_output.c:958-963
-      p.udp = (fl & kCsumUdp) != 0;
-      p.l4_store = ip.l3 + ip.hl + pkthdr_of(m)->csum_data;
-      p.l4_job = (int)jobs.size();
-      jobs.push_back({m, ip.l3 + ip.ip_len, ip.l3 + ip.hl, 0u});
-    }
-    if (fl & kCsumIp) {  // ip_output.c:665-667: ip_sum = 0, then in_cksum(m, hlen)
-      if (ip.l3 + 12 > m->m_len) {
-        p.st = UINET_TX_SKIP;  // header not in the first mbuf: leave it to the stack
-        if (p.l4_job >= 0) jobs.pop_back();
-        p.l4_job = -1;
+  for_chunks(n, [&](int i0, int i1) {
+    for (int i = i0; i < i1; i++) {
+      MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
+      TxPlan& p = plan[(size_t)i];
+      if (!m || !(m->m_flags & kMPktHdr)) {
+        p.st = UINET_TX_SKIP;
         continue;
       }
-      m->m_data[ip.l3 + 10] = 0;
-      m->m_data[ip.l3 + 11] = 0;
-      p.ip_job = (int)jobs.size();
-      jobs.push_back({m, ip.l3 + ip.hl, ip.l3, 0u});
+      const int fl = pkthdr_of(m)->csum_flags;
+      if ((fl & kCsumTso) || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) ||
+          !parse_ip4(m, l2len, &p.ip)) {
+        p.st = UINET_TX_SKIP;
+        continue;
+      }
+      const Ip4& ip = p.ip;
+      if ((fl & kCsumIp) && ip.l3 + 12 > m->m_len) {
+        p.st = UINET_TX_SKIP;  // header not in the first mbuf: leave it to the stack
+        continue;
+      }
+      if (fl & (kCsumTcp | kCsumUdp)) {  // in_delayed_cksum, ip_output.c:958-963
+        p.udp = (fl & kCsumUdp) != 0;
+        p.l4_store = ip.l3 + ip.hl + pkthdr_of(m)->csum_data;
+        p.l4_job = true;
+        jobs[2 * (size_t)i + 1] = {m, ip.l3 + ip.ip_len, ip.l3 + ip.hl, 0u};
+      }
+      if (fl & kCsumIp) {  // ip_output.c:665-667: ip_sum = 0, then in_cksum(m, hlen)
+        m->m_data[ip.l3 + 10] = 0;
+        m->m_data[ip.l3 + 11] = 0;
+        p.ip_job = true;
+        jobs[2 * (size_t)i] = {m, ip.l3 + ip.hl, ip.l3, 0u};
+      }
     }
-  }
+  });
   std::vector<uint16_t>& res = t_res;
   res.resize(jobs.size());
   const int rc = run_jobs(jobs.data(), (int)jobs.size(), res.data());
   if (rc) return rc;
-  for (int i = 0; i < n; i++) {
-    TxPlan& p = plan[(size_t)i];
-    MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
-    if (p.l4_job >= 0) {
-      uint16_t c = res[(size_t)p.l4_job];
-      if (p.udp && c == 0) c = 0xffff;  // ip_output.c:962-963
-      if (p.l4_store + 2 > m->m_len) {
-        p.st |= UINET_TX_L4_LOST;  // ip_output.c:966-974: the reference gives up too
-      } else {
-        memcpy(m->m_data + p.l4_store, &c, 2);
-        p.st |= UINET_TX_L4;
+  for_chunks(n, [&](int i0, int i1) {
+    for (int i = i0; i < i1; i++) {
+      TxPlan& p = plan[(size_t)i];
+      MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
+      if (p.l4_job) {
+        uint16_t c = res[2 * (size_t)i + 1];
+        if (p.udp && c == 0) c = 0xffff;  // ip_output.c:962-963
+        if (p.l4_store + 2 > m->m_len) {
+          p.st |= UINET_TX_L4_LOST;  // ip_output.c:966-974: the reference gives up too
+        } else {
+          memcpy(m->m_data + p.l4_store, &c, 2);
+          p.st |= UINET_TX_L4;
+        }
+        pkthdr_of(m)->csum_flags &= ~(kCsumTcp | kCsumUdp);
       }
-      pkthdr_of(m)->csum_flags &= ~(kCsumTcp | kCsumUdp);
+      if (p.ip_job) {
+        const uint16_t c = res[2 * (size_t)i];
+        memcpy(m->m_data + p.ip.l3 + 10, &c, 2);
+        p.st |= UINET_TX_IP;
+        pkthdr_of(m)->csum_flags &= ~kCsumIp;
+      }
+      if (status) status[i] = p.st;
     }
-    if (p.ip_job >= 0) {
-      const uint16_t c = res[(size_t)p.ip_job];
-      memcpy(m->m_data + p.ip.l3 + 10, &c, 2);
-      p.st |= UINET_TX_IP;
-      pkthdr_of(m)->csum_flags &= ~kCsumIp;
-    }
-    if (status) status[i] = p.st;
-  }
+  });
   return UINET_CKSUM_OK;
 }
 

@@ -168,3 +168,40 @@ def test_offload_gpu_empty_and_bad_args(torch_dev):
     # NULL packets are skipped, not dereferenced
     assert u.tx_offload(np.zeros(3, np.uint64)).tolist() == [TX_SKIP] * 3
     assert u.rx_offload(np.zeros(3, np.uint64)).tolist() == [0] * 3
+
+
+def _pcap_rx(frames):
+    """Every frame of the reference's passive_extract_test.pcap as received:
+    one cluster each, m_data at the Ethernet header."""
+    from libuinet_amd.mbuf import MbufChains, aligned_empty
+
+    arena = aligned_empty(2048 * len(frames) + 64)
+    for i, f in enumerate(frames):
+        arena[2048 * i:2048 * i + len(f)] = np.frombuffer(f, np.uint8)
+    return MbufChains.contiguous(arena, 2048 * np.arange(len(frames)),
+                                 [len(f) for f in frames]), arena
+
+
+def test_pcap_rx_offload_oracle(ora, pcap_frames):
+    """The reference's own capture through the RX hook (SURVEY.md 8f item 3,
+    without libpcap): every IPv4/TCP frame is marked IP-valid and
+    data-valid with csum_data 0xffff, exactly what if_loop.c:96-101 sets."""
+    rx, _ = _pcap_rx(pcap_frames)
+    st = ora.rx_offload(rx.heads)
+    fl, cd = pkthdr_fields(rx)
+    tcp = (st & RX_L4) != 0
+    assert tcp.sum() >= 113
+    assert ((st[tcp] & (RX_IPV4 | RX_IP_OK | RX_L4 | RX_L4_OK)) == 0x0F).all()
+    assert (cd[tcp] == 0xFFFF).all()
+    assert ((fl[tcp] & 0xF00) == 0xF00).all()
+
+
+@pytest.mark.gpu
+def test_pcap_rx_offload_gpu(torch_dev, ora, pcap_frames):
+    import libuinet_amd as u
+
+    rx_g, _ = _pcap_rx(pcap_frames)
+    rx_o, _ = _pcap_rx(pcap_frames)
+    np.testing.assert_array_equal(u.rx_offload(rx_g.heads), ora.rx_offload(rx_o.heads))
+    for x, y in zip(pkthdr_fields(rx_g), pkthdr_fields(rx_o)):
+        np.testing.assert_array_equal(x, y)

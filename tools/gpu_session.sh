@@ -40,5 +40,6 @@ fi
 if [[ $WHAT == all || $WHAT == host || $WHAT == tests+host ]]; then
   run echo_replay 600 python tools/echo_replay.py
   run host_path 600 python tools/host_path.py
+  run offload_rate 600 python tools/offload_rate.py
 fi
 echo "== done"
