@@ -35,6 +35,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "cksum_device.h"
 
 namespace uinet {
@@ -79,6 +81,7 @@ __global__ __launch_bounds__(kBlock) void k_chains(const uint8_t* __restrict__ b
 
 constexpr int kWaves = kBlock / 64;
 constexpr int kLongU = 4;  // chunks in flight per lane on a long segment
+constexpr uint32_t kListMax = 1024;  // longest segment (chunks) the chunk list takes
 
 template <int kPass, int kTile>
 __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restrict__ base,
@@ -93,7 +96,9 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
   static_assert(kTile >= 1 && kTile <= 64, "a tile's packets are one per lane");
   constexpr int kWin = 64 * kPass;  // chunks per batch of passes
   __shared__ MaskLut lut;
-  __shared__ unsigned long long lds_acc[kWaves][kTile];
+  // per packet two sums: bytes at even / odd logical-vs-address parity
+  // (index meta = slot * 2 + rot); the odd one is byte-rotated once at the end
+  __shared__ unsigned long long lds_acc[kWaves][2 * kTile];
   __shared__ uint32_t lds_pkmark[kWaves][64];   // packet-start markers (slot + 1)
   __shared__ uint8_t lds_mark[kWaves][kWin];     // segment-start markers (lane + 1)
   lut.init();
@@ -115,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
     const uint32_t k_len = (lane < np) ? (plen ? plen[P0 + lane] : 0xffffffffu) : 0u;
     const uint32_t S0 = __builtin_amdgcn_readfirstlane(ps);
     const uint32_t S1 = __builtin_amdgcn_readlane(ps, np);
-    if (lane < kTile) acc[lane] = 0;
+    if (lane < 2 * kTile) acc[lane] = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     uint32_t carry_slot1 = 0;  // slot + 1 of the last segment of the previous round
     uint32_t carry_pos = 0;    // chain offset just past that segment
@@ -161,7 +166,8 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
       const uint32_t span = (eff << 4) | head;  // eff < 2^28
       const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
       // --- long segments: one wave-wide span each -------------------------
-      const bool is_long = long_ch != 0 && nch >= long_ch;
+      // (and any segment too long for the chunk list's 20-bit offsets)
+      const bool is_long = nch >= kListMax || (long_ch != 0 && nch >= long_ch);
       for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
         const int s = (int)__builtin_ctzll(lm);
         const uint32_t sp = __builtin_amdgcn_readlane(span, s);
@@ -186,74 +192,103 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
             }
           }
         }
-        uint32_t x = fold16_32(__builtin_amdgcn_readlane(wave_scan<0, false>(fold16(lsum), 0u), 63));
-        if (mts & 1) x = rot8(x);
-        if (lane == 0) atomicAdd(&acc[mts >> 1], (unsigned long long)x);
+        const uint32_t x = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(lsum), 0u), 63);
+        if (lane == 0) atomicAdd(&acc[mts], (unsigned long long)x);
       }
       const uint32_t nch_l = is_long ? 0u : nch;  // the chunk list holds the rest
       const uint32_t ci = wave_scan<0, false>(nch_l, 0u);
       const uint32_t cst = ci - nch_l;  // first chunk of each segment in the round's list
-      const uint32_t C = __builtin_amdgcn_readlane(ci, 63);
+      const uint32_t C = __builtin_amdgcn_readlane(ci, 63);  // < 64 * kListMax
+      // Per list segment, what a chunk c of the list needs:
+      //   address  sbase + (dkr + 16 c) with a 32-bit offset when the round's
+      //            list segments lie within a 4 GiB window (sbase scalar), else
+      //            base + dk + 16 c in 64 bits (dk = c0 - 16 cst)
+      //   bytes    [q - 16 c, q + eff - 16 c) of the chunk   (q = head + 16 cst)
+      //   meta     slot, rotation
+      const uint32_t q0 = head + 16u * cst;  // < 2^20
+      const uint32_t recA = q0 | (meta << 20);
+      const uint32_t recB = q0 + eff;
+      const uint64_t dk = c0 - 16ull * cst;
+      const uint64_t lm_list = __ballot(nch_l != 0);
+      const int lf = lm_list ? (int)__builtin_ctzll(lm_list) : 0;
+      const uint64_t R0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(c0 >> 32), lf) << 32) |
+                          __builtin_amdgcn_readlane((uint32_t)c0, lf);
+      const uint64_t rel = c0 - R0 + (1ull << 31);  // R0 - 2 GiB .. R0 + 2 GiB
+      const bool window = __ballot(nch_l != 0 && rel >= (1ull << 32) - (1ull << 16)) == 0;
+      const uint8_t* sbase = base + (R0 - (1ull << 31));
+      const uint32_t dkr = (uint32_t)rel - 16u * cst;  // mod 2^32; + 16 c lands in range
       // --- data: batches of kPass passes over the round's chunk list ------
-      uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the pass
-      for (uint32_t b = 0; b < C; b += kWin) {
-        const bool mk = nch_l != 0 && cst >= b && cst < b + kWin;
-        if (mk) mark[cst - b] = (uint8_t)(lane + 1);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        u32x4 v[kPass];
-        int s_lo[kPass], s_hi[kPass];
-        uint32_t mt[kPass];
-        // segment starts of all passes at once: independent max-scans, then
-        // the carries as a scalar prefix max (seg1 never decreases)
-        uint32_t sc1[kPass];
+      auto sweep = [&](auto kWindow) {
+        uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the pass
+        for (uint32_t b = 0; b < C; b += kWin) {
+          const bool mk = nch_l != 0 && cst >= b && cst < b + kWin;
+          if (mk) mark[cst - b] = (uint8_t)(lane + 1);
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          u32x4 v[kPass];
+          int s_lo[kPass], s_hi[kPass];
+          uint32_t mt[kPass];
+          // segment starts of all passes at once: independent max-scans, then
+          // the carries as a scalar prefix max (seg1 never decreases)
+          uint32_t sc1[kPass];
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) sc1[q] = mark[q * 64 + lane];
+          for (int q = 0; q < kPass; ++q) sc1[q] = mark[q * 64 + lane];
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) sc1[q] = wave_scan<1, false>(sc1[q], 0u);
+          for (int q = 0; q < kPass; ++q) sc1[q] = wave_scan<1, false>(sc1[q], 0u);
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) {
-          const uint32_t last = __builtin_amdgcn_readlane(sc1[q], 63);
-          sc1[q] = max(sc1[q], carry_seg1);
-          carry_seg1 = max(carry_seg1, last);
-        }
+          for (int q = 0; q < kPass; ++q) {
+            const uint32_t last = __builtin_amdgcn_readlane(sc1[q], 63);
+            sc1[q] = max(sc1[q], carry_seg1);
+            carry_seg1 = max(carry_seg1, last);
+          }
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) {
-          const uint32_t c = b + (uint32_t)(q * 64 + lane);
-          const bool in = c < C;
-          const int seg = (int)sc1[q] - 1;
-          // Cross-lane reads stay outside any condition: a ds_bpermute under
-          // a partial exec mask reads 0 from the inactive source lanes.
-          const uint32_t cst_seg = (uint32_t)__shfl(cst, seg);
-          const uint32_t k = in ? c - cst_seg : 0u;  // past the end: chunk 0, masked
-          const uint64_t cbase = ((uint64_t)(uint32_t)__shfl(c0_hi, seg) << 32) |
-                                 (uint32_t)__shfl(c0_lo, seg);
-          const uint32_t sp = __shfl(span, seg);
-          mt[q] = __shfl(meta, seg);
-          const int h = (int)(sp & 15), e = (int)(sp >> 4);
-          s_lo[q] = h - 16 * (int)k;
-          s_hi[q] = in ? h + e - 16 * (int)k : s_lo[q];
-          v[q] = load_chunk(base + cbase + 16ull * k);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (mk) mark[cst - b] = 0;
+          for (int q = 0; q < kPass; ++q) {
+            const uint32_t c = b + (uint32_t)(q * 64 + lane);
+            const bool in = c < C;
+            const uint32_t cc = in ? c : C - 1;  // past the end: the last chunk, masked
+            const int seg = (int)sc1[q] - 1;
+            // Cross-lane reads stay outside any condition: a ds_bpermute under
+            // a partial exec mask reads 0 from the inactive source lanes.
+            const uint32_t a = (uint32_t)__shfl(recA, seg);
+            const uint32_t bq = (uint32_t)__shfl(recB, seg);
+            mt[q] = a >> 20;
+            const int base16 = 16 * (int)c;
+            s_lo[q] = (int)(a & 0xfffffu) - base16;
+            s_hi[q] = in ? (int)bq - base16 : s_lo[q];
+            if constexpr (decltype(kWindow)::value) {
+              const uint32_t d = (uint32_t)__shfl(dkr, seg);
+              v[q] = load_chunk(sbase + (d + 16u * cc));
+            } else {
+              const uint32_t lo32 = (uint32_t)__shfl((uint32_t)dk, seg);
+              const uint32_t hi32 = (uint32_t)__shfl((uint32_t)(dk >> 32), seg);
+              v[q] = load_chunk(base + ((((uint64_t)hi32 << 32) | lo32) + 16ull * cc));
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          if (mk) mark[cst - b] = 0;
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) {
-          uint32_t w = fold16(lut.sum(v[q], s_lo[q], s_hi[q]));
-          if (mt[q] & 1) w = rot8(w);
-          const uint32_t sl = mt[q] >> 1;
-          const uint32_t P = wave_scan<0, false>(w, 0u);
-          const uint32_t nx = __shfl_down(sl, 1);
-          if (lane == 63 || nx != sl) {
-            atomicAdd(&acc[sl], (unsigned long long)P);
-            if (lane != 63) atomicAdd(&acc[nx], (unsigned long long)(-(long long)P));
+          for (int q = 0; q < kPass; ++q) {
+            // binned by (slot, rot): runs of equal keys, telescoping +P / -P
+            const uint32_t w = lut.sum_oc(v[q], s_lo[q], s_hi[q]);  // < 2^17
+            const uint32_t sl = mt[q];
+            const uint32_t P = wave_scan<0, false>(w, 0u);          // < 2^23
+            const uint32_t nx = wave_shl1(sl);
+            if (lane == 63 || nx != sl) {
+              atomicAdd(&acc[sl], (unsigned long long)P);
+              if (lane != 63) atomicAdd(&acc[nx], (unsigned long long)(-(long long)P));
+            }
           }
         }
-      }
+      };
+      if (window)
+        sweep(std::true_type());
+      else
+        sweep(std::false_type());
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (lane < np) {
       const uint32_t p = P0 + (uint32_t)lane;
-      out[p] = finish(acc[lane] + (seed ? seed[p] : 0u), flags);
+      const uint32_t odd = fold16(acc[2 * lane + 1]);
+      out[p] = finish(acc[2 * lane] + rot8(odd) + (seed ? seed[p] : 0u), flags);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }

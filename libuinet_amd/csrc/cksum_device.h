@@ -86,6 +86,20 @@ struct MaskLut {
   __device__ __forceinline__ uint64_t sum(u32x4 v, int s, int e) const {
     return masked_sum(v, m[clampi(s, 0, 16) * 17 + clampi(e, 0, 16)]);
   }
+  // The same bytes as a 32-bit one's-complement sum (end-around carry) of
+  // the masked words, folded once: < 2^17, congruent to sum() mod 65535
+  // (2^32 - 1 = 65535 * 65537) and zero only when sum() is.  A carry out of
+  // an add-with-carry always leaves <= 0xfffffffe, so the last carry-in never
+  // overflows.
+  __device__ __forceinline__ uint32_t sum_oc(u32x4 v, int s, int e) const {
+    const u32x4 k = m[clampi(s, 0, 16) * 17 + clampi(e, 0, 16)];
+    unsigned c0, c1, c2, c3;
+    unsigned t = __builtin_addc(v.x & k.x, v.y & k.y, 0u, &c0);
+    t = __builtin_addc(t, v.z & k.z, c0, &c1);
+    t = __builtin_addc(t, v.w & k.w, c1, &c2);
+    t = __builtin_addc(t, 0u, c2, &c3);
+    return (t & 0xffff) + (t >> 16);
+  }
 };
 
 __device__ __forceinline__ u32x4 load_chunk(const uint8_t* p) {
@@ -196,6 +210,12 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t key) {
   UINET_DPP_STEP(0x143, 0xc)  // row_bcast:31 -> rows 2, 3
 #undef UINET_DPP_STEP
   return x;
+}
+
+// Lane i gets lane i+1's x (DPP wave_shl:1, a gfx9-family control; lane 63
+// gets 0).  Needs all 64 lanes active.
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
 }
 
 }  // namespace uinet
