@@ -112,6 +112,8 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
   uint8_t* mark = lds_mark[wid];
   const uint32_t tiles = (n + kTile - 1) / kTile;
   const uint32_t wstride = gridDim.x * kWaves;
+  // (plain block order: the XCD-banded order of the span kernels measured
+  // 1-3 % slower here, profiles/r01/ab/)
   for (uint32_t t = blockIdx.x * kWaves + wid; t < tiles; t += wstride) {
     const uint32_t P0 = t * kTile;
     const int np = (int)min((uint32_t)kTile, n - P0);

@@ -212,6 +212,17 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t key) {
   return x;
 }
 
+// The hardware deals blocks round-robin over the 8 XCDs (block b on XCD
+// b % 8), each with its own L2.  With `remap`, block b takes logical id
+// (b % 8) * (grid / 8) + b / 8, so an XCD's blocks work on one contiguous band
+// of packets (tiles) and the cache line two neighbours share is fetched
+// into one L2 instead of two.
+__device__ __forceinline__ uint32_t logical_block(uint32_t remap) {
+  const uint32_t b = blockIdx.x, per = gridDim.x / 8;
+  if (!remap || b >= 8 * per) return b;
+  return (b % 8) * per + b / 8;
+}
+
 // Lane i gets lane i+1's x (DPP wave_shl:1, a gfx9-family control; lane 63
 // gets 0).  Needs all 64 lanes active.
 __device__ __forceinline__ uint32_t wave_shl1(uint32_t x) {

@@ -19,6 +19,7 @@ struct Tuning {
   int chains_long;     // flat chains: segments of >= this many 16-B chunks stream
                        // wave-wide (0 = never)
   int chains_tile;     // flat chains: packets per wave tile, 0 = auto, 8, 32
+  int xcd_remap;       // span kernels: XCD-banded block order (0/1)
 };
 const Tuning& tuning();
 

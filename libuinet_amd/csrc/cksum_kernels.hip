@@ -36,11 +36,11 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
                                                  const uint8_t* __restrict__ parity,
                                                  uint64_t pkt_stride, uint32_t fixed_len,
                                                  uint16_t* __restrict__ out, uint32_t n,
-                                                 uint32_t flags) {
+                                                 uint32_t flags, uint32_t remap) {
   constexpr uint32_t kGroups = kBlock / G;
   const int gl = threadIdx.x & (G - 1);
   const uint32_t stride = gridDim.x * kGroups;
-  uint32_t p = blockIdx.x * kGroups + threadIdx.x / G;
+  uint32_t p = logical_block(remap) * kGroups + threadIdx.x / G;
   if (p >= n) return;  // whole groups leave together
   uint64_t o = kStrided ? (uint64_t)p * pkt_stride : off[p];
   uint32_t l = kStrided ? fixed_len : len[p];
@@ -124,7 +124,7 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
 #define L(G, U)                                                                    \
   hipLaunchKernelGGL((k_spans<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,  \
                      static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, out, \
-                     n, flags)
+                     n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
@@ -138,7 +138,7 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
 #define L(G, U)                                                                     \
   hipLaunchKernelGGL((k_spans<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,    \
                      static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
-                     pkt_stride, len, out, n, flags)
+                     pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
