@@ -195,21 +195,31 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # UINET_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
+    # one GPU (CI / 1-GPU boxes); the real runs use RCCL, one rank per GPU.
+    backend = os.environ.get("UINET_BENCH_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     import libuinet_amd as u
-    from libuinet_amd.dist import gather_results
+    from libuinet_amd.dist import ResultGather
 
     if not u.device_ok():
         raise SystemExit("bench: no gfx950 device visible")
     w = build_workload(args.config, args.packets, rank)
     n = w["n"]
-    out = torch.empty(n, dtype=torch.uint16, device="cuda")
+    # two result buffers: step k's gather overlaps step k+1's kernel (N > 1)
+    outs = [torch.empty(n, dtype=torch.uint16, device="cuda") for _ in range(2)]
+    out = outs[0]
     stream = torch.cuda.current_stream()
-    launch = make_launch(args.config, w, args.api, out)
+    launches = [make_launch(args.config, w, args.api, o) for o in outs]
     counts = [n] * world
+    rg = ResultGather(counts, "cuda") if world > 1 else None
     K, Wm = args.steps, args.warmup
     # Kernel time from HIP events on the launch stream.  At N = 1 a step IS
     # one launch, so one event pair brackets the K back-to-back launches (no
@@ -219,17 +229,22 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(K if per_launch else 1)]
 
-    def step(k=None):
+    def step(k=None, i=0):
+        slot = i & 1
+        if rg is not None:
+            rg.wait(slot)  # the gather that last read this buffer is done
         if per_launch and k is not None:
             ev[k][0].record(stream)
-        launch(stream)
+        launches[slot](stream)
         if per_launch and k is not None:
             ev[k][1].record(stream)
-        if world > 1:
-            gather_results(out, counts)
+        if rg is not None:
+            rg.start(outs[slot], slot)  # the one exchange: u16 results -> rank 0
 
-    for _ in range(Wm):
-        step()
+    for i in range(Wm):
+        step(None, i)
+    if rg is not None:
+        rg.wait_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -238,16 +253,19 @@ def main():
     if not per_launch:
         ev[0][0].record(stream)
     for k in range(K):
-        step(k)
+        step(k, k)
     if not per_launch:
         ev[0][1].record(stream)
+    if rg is not None:
+        rg.wait_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if per_launch:
@@ -281,8 +299,9 @@ def main():
                 "algorithmic_bytes_per_gpu": w["bytes"],
                 "api": {"spans": "uinet_cksum_spans", "strided": "uinet_cksum_strided"}[args.api]
                 if args.config not in CHAIN_CONFIGS else "uinet_cksum_chains",
-                "parallelism": f"dp{world} packet shards" + (" + RCCL gather of u16 results"
-                                                             if world > 1 else ""),
+                "parallelism": f"dp{world} packet shards" + (
+                    f" + {'RCCL' if backend == 'nccl' else backend} gather of u16 results, "
+                    "overlapped with the next step's kernel" if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -301,7 +320,7 @@ def main():
             result["host_resident"] = host_path_rate(args, w)
     if world == 1 and rank == 0 and args.cpu_baseline == "auto":
         torch.cuda.synchronize()
-        gpu_out = out.cpu().view(torch.int16).numpy().view(np.uint16)
+        gpu_out = outs[(K - 1) & 1].cpu().view(torch.int16).numpy().view(np.uint16)
         result["cpu_baseline"] = cpu_baseline(args.config, w, gpu_out, args.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -44,7 +44,11 @@ def gather_results(local, counts, group=None, dst: int = 0):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     cmax = 2 * int(max(counts))
-    # Moved as bytes: every backend (gloo, RCCL) carries uint8.
+    # Moved as bytes: every backend (gloo, RCCL) carries uint8.  gloo's
+    # gather takes host tensors only.
+    home = local.device
+    if dist.get_backend(group) == "gloo" and local.is_cuda:
+        local = local.cpu()
     send = local.contiguous().view(torch.uint8)
     if send.numel() < cmax:
         pad = torch.zeros(cmax, dtype=torch.uint8, device=send.device)
@@ -55,4 +59,63 @@ def gather_results(local, counts, group=None, dst: int = 0):
     dist.gather(send, gather_list=gl, dst=dst, group=group)
     if rank != dst:
         return None
-    return torch.cat([g[: 2 * int(c)] for g, c in zip(gl, counts)]).view(local.dtype)
+    return torch.cat([g[: 2 * int(c)] for g, c in zip(gl, counts)]).view(local.dtype).to(home)
+
+
+class ResultGather:
+    """The per-step gather of u16 results, asynchronous and double-buffered:
+    step k's gather runs on the collective stream while step k+1's kernel
+    runs on the compute stream (xGMI traffic and an HBM-bound fold overlap);
+    a slot is only rewritten after its previous gather completed.
+
+    ``start(local, slot)`` enqueues the gather of ``local`` (the rank's
+    results, written on the current stream); ``wait(slot)`` orders the
+    current stream after it; ``result(slot)`` is the concatenated array on
+    ``dst`` (None elsewhere) once waited."""
+
+    def __init__(self, counts, device, group=None, dst: int = 0, depth: int = 2):
+        import torch
+        import torch.distributed as dist
+
+        self.group, self.dst = group, dst
+        self.counts = [int(c) for c in counts]
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.host = dist.get_backend(group) == "gloo"
+        dev = torch.device("cpu") if self.host else torch.device(device)
+        self.cmax = 2 * max(self.counts)
+        self.pad = [torch.zeros(self.cmax, dtype=torch.uint8, device=dev) for _ in range(depth)]
+        self.recv = [[torch.empty(self.cmax, dtype=torch.uint8, device=dev)
+                      for _ in range(self.world)] if self.rank == dst else None
+                     for _ in range(depth)]
+        self.work = [None] * depth
+
+    def start(self, local, slot: int):
+        import torch.distributed as dist
+
+        self.wait(slot)
+        send = local.contiguous().view(__import__("torch").uint8)
+        if self.host and send.is_cuda:
+            send = send.cpu()
+        if send.numel() < self.cmax or send.device != self.pad[slot].device:
+            self.pad[slot][: send.numel()].copy_(send)
+            send = self.pad[slot]
+        self.work[slot] = dist.gather(send, gather_list=self.recv[slot], dst=self.dst,
+                                      group=self.group, async_op=True)
+
+    def wait(self, slot: int) -> None:
+        if self.work[slot] is not None:
+            self.work[slot].wait()
+            self.work[slot] = None
+
+    def wait_all(self) -> None:
+        for s in range(len(self.work)):
+            self.wait(s)
+
+    def result(self, slot: int, dtype=None):
+        import torch
+
+        if self.rank != self.dst:
+            return None
+        out = torch.cat([g[: 2 * c] for g, c in zip(self.recv[slot], self.counts)])
+        return out.view(dtype or torch.int16)

@@ -75,3 +75,46 @@ def test_gather_world2_gloo(tmp_path):
 def test_shard_range_matches_bounds():
     b = shard_bounds(1001, 4)
     assert [shard_range(1001, r, 4) for r in range(4)] == [(int(b[r]), int(b[r + 1])) for r in range(4)]
+
+
+def _worker_async(rank, world, port, result_path):
+    import torch
+    import torch.distributed as dist
+
+    from libuinet_amd.dist import ResultGather
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        counts = [3, 5, 4][:world]
+        rg = ResultGather(counts, "cpu")
+        got = []
+        for step in range(5):  # the bench's double-buffered pattern
+            slot = step & 1
+            rg.wait(slot)
+            local = torch.arange(counts[rank], dtype=torch.int16) + 100 * rank + 1000 * step
+            rg.start(local, slot)
+            if step >= 1:
+                prev = (step - 1) & 1
+                rg.wait(prev)
+                if rank == 0:
+                    got.append(rg.result(prev).numpy().copy())
+        rg.wait_all()
+        if rank == 0:
+            got.append(rg.result(4 & 1).numpy().copy())
+            np.save(result_path, np.stack(got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_async_result_gather_world3_gloo(tmp_path):
+    import torch.multiprocessing as mp
+
+    path = str(tmp_path / "res.npy")
+    mp.spawn(_worker_async, args=(3, _free_port(), path), nprocs=3, join=True)
+    got = np.load(path)
+    for step in range(5):
+        want = np.concatenate([np.arange(c) + 100 * r + 1000 * step
+                               for r, c in enumerate([3, 5, 4])])
+        np.testing.assert_array_equal(got[step], want)
