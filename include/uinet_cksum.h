@@ -44,6 +44,8 @@ extern "C" {
 struct mbuf;
 /* struct ip (sys/netinet/ip.h:49-70): 20 bytes, ip_sum at offset 10. */
 struct ip;
+/* struct ip6_hdr (sys/netinet/ip6.h:74-92): 40 bytes, addresses at 8 / 24. */
+struct ip6_hdr;
 
 /* ------------------------------------------------------------------------ */
 /* 1. Drop-in per-call ABI (sys/amd64/include/in_cksum.h)                    */
@@ -85,6 +87,18 @@ uinet_in_cksum_update(void *ip_hdr)
 	p[0] = (unsigned char)(s >> 8);
 	p[1] = (unsigned char)s;
 }
+
+/* IPv6 (sys/netinet6/in6.h:637-638, compiled
+ * by the reference only with INET6).  in6_cksum.c:150-357: the transport
+ * segment [off, off + len) of the chain (off counts from the chain start,
+ * m_data at a contiguous IPv6 header), seeded with the IPv6 pseudo header
+ * (addresses without their embedded scope zone, htonl(len), nxt); returns
+ * the complemented sum.  The reference panics when the chain is shorter
+ * than off + len; here the chain's bytes are summed as far as they go. */
+int in6_cksum(struct mbuf *m, uint8_t nxt, uint32_t off, uint32_t len);
+/* in6_cksum.c:129-140: folded pseudo-header sum plus csum, NOT complemented. */
+int in6_cksum_pseudo(struct ip6_hdr *ip6, uint32_t len, uint8_t nxt,
+    uint16_t csum);
 
 /* ------------------------------------------------------------------------ */
 /* 2a. Status                                                                */
@@ -177,6 +191,8 @@ int in_cksum_pseudo_header_batch(struct mbuf *const *m, const int *plen,
     const int *off0, const uint32_t *src, const uint32_t *dst,
     const uint8_t *protonum, uint16_t *out, int n);
 int in_cksum_hdr_batch(const struct ip *const *ip, unsigned int *out, int n);
+int in6_cksum_batch(struct mbuf *const *m, const uint8_t *nxt,
+    const uint32_t *off, const uint32_t *len, uint16_t *out, int n);
 
 /* Zero-copy host regions.  Register the host memory that holds packet data
  * (the netmap ring buffers, uinet_if_netmap_host.c:153; the UMA slabs behind

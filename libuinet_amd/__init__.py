@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "in_cksum_skip_batch", "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch",
     "uinet_cksum_register_host", "uinet_cksum_unregister_host",
     "uinet_cksum_rx_offload", "uinet_cksum_tx_offload",
+    "in6_cksum", "in6_cksum_pseudo", "in6_cksum_batch",
 )
 
 # Driver offload status bits (include/uinet_cksum.h section 2d).
@@ -107,6 +108,9 @@ def lib() -> ctypes.CDLL:
         "uinet_cksum_unregister_host": (_i32, [_vp]),
         "uinet_cksum_rx_offload": (_i32, [_vp, _i32, _i32, _vp]),
         "uinet_cksum_tx_offload": (_i32, [_vp, _i32, _i32, _vp]),
+        "in6_cksum": (_i32, [_vp, _u8, _u32, _u32]),
+        "in6_cksum_pseudo": (_i32, [_vp, _u32, _u8, _u16]),
+        "in6_cksum_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -192,6 +196,29 @@ def register_host(buf: np.ndarray) -> None:
 
 def unregister_host(buf: np.ndarray) -> None:
     _check("uinet_cksum_unregister_host", lib().uinet_cksum_unregister_host(buf.ctypes.data))
+
+
+def in6_cksum(m: int, nxt: int, off: int, length: int) -> int:
+    """sys/netinet6/in6_cksum.c:150-357 (per call, a GPU batch of one)."""
+    return lib().in6_cksum(m, nxt, off, length)
+
+
+def in6_cksum_pseudo(ip6: int, length: int, nxt: int, csum: int) -> int:
+    """in6_cksum.c:129-140: folded pseudo-header sum + csum (host fold)."""
+    return lib().in6_cksum_pseudo(ip6, length, nxt, csum)
+
+
+def in6_cksum_batch(heads, nxt, off, length) -> np.ndarray:
+    """in6_cksum(m[i], nxt[i], off[i], len[i]) for a batch, one GPU launch."""
+    heads = np.ascontiguousarray(heads, dtype=np.uint64)
+    n = heads.size
+    nxt = np.ascontiguousarray(np.broadcast_to(nxt, (n,)), dtype=np.uint8)
+    off = np.ascontiguousarray(np.broadcast_to(off, (n,)), dtype=np.uint32)
+    length = np.ascontiguousarray(np.broadcast_to(length, (n,)), dtype=np.uint32)
+    out = np.zeros(n, dtype=np.uint16)
+    _check("in6_cksum_batch", lib().in6_cksum_batch(_ptr(heads), _ptr(nxt), _ptr(off),
+                                                   _ptr(length), _ptr(out), n))
+    return out
 
 
 def rx_offload(heads, l2len: int = -1) -> np.ndarray:

@@ -500,6 +500,27 @@ int run_jobs(const Job* jobs, int n, uint16_t* out) {
 
 namespace {
 
+// ---- IPv6 pseudo header (sys/netinet6/in6_cksum.c:86-126) -------------------
+
+// The zone index KAME embeds in word 1 of link-local unicast and link- /
+// interface-local multicast addresses is left out of the sum
+// (in6_cksum.c:110-124, scope6.c:502-509, netinet6/in6.h:294-356).
+uint64_t in6_scope_word(const uint8_t* a) {
+  const bool ll = a[0] == 0xfe && (a[1] & 0xc0) == 0x80;
+  const bool mc = a[0] == 0xff && ((a[1] & 0x0f) == 0x02 || (a[1] & 0x0f) == 0x01);
+  return (ll || mc) ? (uint64_t)(a[2] | a[3] << 8) : 0;
+}
+
+// htonl(len), three zero bytes, nxt, then the source and destination
+// addresses, all as little-endian 16-bit words; folded.
+uint32_t in6_pseudo_fold(const uint8_t* ip6, uint32_t len, uint8_t nxt) {
+  uint64_t s = ((len >> 24) & 0xff) | ((len >> 16) & 0xff) << 8;
+  s += ((len >> 8) & 0xff) | (len & 0xff) << 8;
+  s += (uint64_t)nxt << 8;
+  for (int i = 0; i < 32; i += 2) s += (uint64_t)(ip6[8 + i] | ip6[8 + i + 1] << 8);
+  return fold16_host(s - in6_scope_word(ip6 + 8) - in6_scope_word(ip6 + 24));
+}
+
 [[noreturn]] void die(const char* fn, int rc) {
   fprintf(stderr, "libuinet_cksum: %s failed: %s (hip error %d: %s)\n", fn,
           uinet_cksum_strerror(rc), t_last_hip, hipGetErrorString((hipError_t)t_last_hip));
@@ -655,6 +676,19 @@ int in_cksum_pseudo_header_batch(struct mbuf* const* m, const int* plen, const i
   });
 }
 
+int in6_cksum_batch(struct mbuf* const* m, const uint8_t* nxt, const uint32_t* off,
+                    const uint32_t* len, uint16_t* out, int n) {
+  if (n > 0 && (!m || !nxt || !off || !len || !out)) return UINET_CKSUM_EINVAL;
+  for (int i = 0; i < n; i++)  // the header is read on the host; off + len fits an int
+    if (!m[i] || (uint64_t)off[i] + len[i] > 0x7fffffffull) return UINET_CKSUM_EINVAL;
+  return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
+    // in6_cksum.c:208-350: off counts from the chain start, then len bytes
+    const MbufHdr* mm = reinterpret_cast<const MbufHdr*>(m[i]);
+    w.walk_skip(mm, (int)(off[i] + len[i]), (int)off[i]);
+    return in6_pseudo_fold(mm->m_data, len[i], nxt[i]);  // "contiguous IP6 header"
+  });
+}
+
 int in_cksum_hdr_batch(const struct ip* const* ip, unsigned int* out, int n) {
   if (n > 0 && (!ip || !out)) return UINET_CKSUM_EINVAL;
   return run_host_batch(n, 0, nullptr, out, [&](int i, PacketWalk& w) -> uint32_t {
@@ -690,6 +724,21 @@ unsigned int in_cksum_hdr(const struct ip* ip) {
   const int rc = in_cksum_hdr_batch(&ip, &r, 1);
   if (rc) die("in_cksum_hdr", rc);
   return r;
+}
+
+// sys/netinet6/in6.h:638, in6_cksum.c:150-357.
+int in6_cksum(struct mbuf* m, uint8_t nxt, uint32_t off, uint32_t len) {
+  uint16_t r = 0;
+  const int rc = in6_cksum_batch(&m, &nxt, &off, &len, &r, 1);
+  if (rc) die("in6_cksum", rc);
+  return r;
+}
+
+// in6.h:637, in6_cksum.c:129-140: 36 header bytes, no payload -- a host fold.
+int in6_cksum_pseudo(struct ip6_hdr* ip6, uint32_t len, uint8_t nxt, uint16_t csum) {
+  const uint8_t* a = reinterpret_cast<const uint8_t*>(ip6);
+  uint64_t s = (uint64_t)in6_pseudo_fold(a, len, nxt) + csum;
+  return (int)fold16_host(s);
 }
 
 // in_pseudo / in_addword fold three or two register values -- no packet

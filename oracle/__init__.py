@@ -61,6 +61,8 @@ class Oracle:
             "oracle_cksum_pseudo_header_batch": (None, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32]),
             "oracle_cksum_hdr_batch": (None, [_vp, _vp, _i32]),
             "oracle_rx_offload": (None, [_vp, _i32, _i32, _vp]),
+            "oracle_in6_cksum_pseudo": (_i32, [_vp, _u32, _u8, _u16]),
+            "oracle_in6_cksum_batch": (None, [_vp, _vp, _vp, _vp, _vp, _i32]),
             "oracle_tx_offload": (None, [_vp, _i32, _i32, _vp]),
         }
         for name, (res, args) in sig.items():
@@ -108,6 +110,18 @@ class Oracle:
         out = np.zeros(ips.size, np.uint32)
         self.L.oracle_cksum_hdr_batch(_p(ips), _p(out), ips.size)
         return out
+
+    def in6_cksum_batch(self, heads, nxt, off, length) -> np.ndarray:
+        """in6_cksum(m, nxt, off, len) per packet (sys/netinet6/in6_cksum.c)."""
+        heads = _c(heads, np.uint64)
+        n = heads.size
+        arrs = [_c(nxt, np.uint8, n), _c(off, np.uint32, n), _c(length, np.uint32, n)]
+        out = np.zeros(n, np.uint16)
+        self.L.oracle_in6_cksum_batch(_p(heads), *[_p(a) for a in arrs], _p(out), n)
+        return out
+
+    def in6_cksum_pseudo(self, ip6: int, length: int, nxt: int, csum: int) -> int:
+        return self.L.oracle_in6_cksum_pseudo(ip6, length, nxt, csum)
 
     def rx_offload(self, heads, l2len: int = -1) -> np.ndarray:
         """offload_oracle.c: the RX hook restated packet by packet (marks pkthdrs)."""

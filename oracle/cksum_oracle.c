@@ -14,6 +14,7 @@
  *   sys/amd64/amd64/in_cksum.c:241-276  in_cksum_pseudo_header
  *   sys/amd64/amd64/in_cksum.c:278-285  in_cksum_hdr
  *   sys/netinet/ip_output.c:962-963     UDP "0 -> 0xffff" rule (caller side)
+ *   sys/netinet6/in6_cksum.c:86-357     in6_cksum / in6_cksum_pseudo (IPv6)
  *
  * Parity is pinned by tests/golden/ (vectors produced by oracle/_ref, the
  * reference object compiled from /root/reference/sys/amd64/amd64/in_cksum.c
@@ -175,6 +176,78 @@ uint16_t
 oracle_in_addword(uint16_t a, uint16_t b)
 {
 	return (uint16_t)fold16((uint64_t)a + b);
+}
+
+/* ---- IPv6 (sys/netinet6/in6_cksum.c) ------------------------------------ */
+
+/* The zone index KAME embeds in word 1 of a link-local unicast or a link- /
+ * interface-local multicast address; in6_cksum leaves it out of the sum
+ * (in6_cksum.c:110-124 with scope6.c:502-509, netinet6/in6.h:294-356). */
+static uint64_t
+in6_scope_word(const uint8_t *a)
+{
+	int ll = a[0] == 0xfe && (a[1] & 0xc0) == 0x80;
+	int mc = a[0] == 0xff && ((a[1] & 0x0f) == 0x02 || (a[1] & 0x0f) == 0x01);
+
+	return (ll || mc) ? (uint64_t)(a[2] | a[3] << 8) : 0;
+}
+
+/* in6_cksum.c:86-126: the pseudo header (htonl(len), three zero bytes,
+ * nxt) and both addresses as little-endian 16-bit words, minus the embedded
+ * scopes.  Unfolded. */
+static uint64_t
+in6_pseudo_sum(const uint8_t *ip6, uint32_t len, uint8_t nxt)
+{
+	uint64_t s = ((len >> 24) & 0xff) | ((len >> 16) & 0xff) << 8;
+	int i;
+
+	s += ((len >> 8) & 0xff) | (len & 0xff) << 8;
+	s += (uint64_t)nxt << 8;
+	for (i = 0; i < 32; i += 2)
+		s += (uint64_t)(ip6[8 + i] | ip6[8 + i + 1] << 8);
+	return s - in6_scope_word(ip6 + 8) - in6_scope_word(ip6 + 24);
+}
+
+int
+oracle_in6_cksum_pseudo(const void *ip6, uint32_t len, uint8_t nxt, uint16_t csum)
+{
+	/* in6_cksum.c:129-140: REDUCE, not complemented */
+	return (int)fold16(in6_pseudo_sum(ip6, len, nxt) + csum);
+}
+
+uint16_t
+oracle_in6_cksum(const struct oracle_mbuf *m, uint8_t nxt, uint32_t off, uint32_t len)
+{
+	/* in6_cksum.c:150-357: "m MUST contain a contiguous IP6 header"; off
+	 * counts from the chain start, len bytes of transport segment follow. */
+	struct walk w = { in6_pseudo_sum((const uint8_t *)m->m_data, len, nxt), 0, (long)len };
+
+	/* :208-214 skip whole mbufs, then :215-219 the rest of the first one */
+	while (off > 0 && m) {
+		if ((uint32_t)m->m_len <= off) {
+			off -= (uint32_t)m->m_len;
+			m = m->m_next;
+			continue;
+		}
+		break;
+	}
+	if (m) {
+		take_piece(&w, (const uint8_t *)m->m_data + off, (long)m->m_len - off);
+		/* :292-350 the following mbufs, zero-length ones passed over;
+		 * running out of data panics there (:351-352) */
+		take_rest(&w, m->m_next);
+	}
+	return (uint16_t)(~fold16(w.sum) & 0xffff);
+}
+
+void
+oracle_in6_cksum_batch(struct oracle_mbuf *const *m, const uint8_t *nxt,
+    const uint32_t *off, const uint32_t *len, uint16_t *out, int n)
+{
+	int i;
+
+	for (i = 0; i < n; i++)
+		out[i] = oracle_in6_cksum(m[i], nxt[i], off[i], len[i]);
 }
 
 /* ---- flat batch helpers (what the GPU descriptor APIs compute) ---------- */

@@ -43,6 +43,13 @@ void oracle_cksum_pseudo_header_batch(struct oracle_mbuf *const *m,
     const uint32_t *dst, const uint8_t *proto, uint16_t *out, int n);
 void oracle_cksum_hdr_batch(const void *const *ip, unsigned *out, int n);
 
+/* IPv6: sys/netinet6/in6_cksum.c */
+uint16_t oracle_in6_cksum(const struct oracle_mbuf *m, uint8_t nxt, uint32_t off,
+    uint32_t len);
+int oracle_in6_cksum_pseudo(const void *ip6, uint32_t len, uint8_t nxt, uint16_t csum);
+void oracle_in6_cksum_batch(struct oracle_mbuf *const *m, const uint8_t *nxt,
+    const uint32_t *off, const uint32_t *len, uint16_t *out, int n);
+
 /* offload_oracle.c: the driver batch offload hooks, restated packet by
  * packet (mutates pkthdr csum fields, and packet bytes on TX). */
 void oracle_rx_offload(struct oracle_mbuf *const *m, int n, int l2len,
