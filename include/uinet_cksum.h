@@ -130,12 +130,15 @@ int uinet_cksum_device_ok(void);
  *   "chains_tile"     packets per wave in the chain kernel: 0 = auto, 8, 32
  *   "xcd_remap"       span kernels: give each XCD a contiguous band of
  *                     packets (1, default) or plain block order (0)
+ *   "spans_lut"       span kernels: LDS mask table + one's-complement chunk
+ *                     sums (1, default) or register masks + 64-bit sums (0)
  *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
  *                     1..64 (default min(8, hardware threads))
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
  * (serial|flat), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
- * UINET_CKSUM_CHAINS_TILE, UINET_CKSUM_XCD_REMAP and UINET_CKSUM_HOST_THREADS set
+ * UINET_CKSUM_CHAINS_TILE, UINET_CKSUM_XCD_REMAP, UINET_CKSUM_SPANS_LUT and
+ * UINET_CKSUM_HOST_THREADS set
  * the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 

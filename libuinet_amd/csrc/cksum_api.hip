@@ -51,7 +51,7 @@ int check_launch() { return record_hip(hipGetLastError()); }
 static Tuning& tuning_rw() {
   static Tuning t = [] {
     const unsigned hw = std::thread::hardware_concurrency();
-    Tuning x{0, 0, 2, (int)std::min(8u, hw ? hw : 1u), 128, 0, 1};
+    Tuning x{0, 0, 2, (int)std::min(8u, hw ? hw : 1u), 128, 0, 1, 1};
     if (const char* e = getenv("UINET_CKSUM_BLOCKS_PER_CU")) {
       const int v = atoi(e);
       x.blocks_per_cu = (v > 0 && v <= 4096) ? v : 0;
@@ -70,6 +70,7 @@ static Tuning& tuning_rw() {
       if (v == 0 || v == 8 || v == 32) x.chains_tile = v;
     }
     if (const char* e = getenv("UINET_CKSUM_XCD_REMAP")) x.xcd_remap = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("UINET_CKSUM_SPANS_LUT")) x.spans_lut = atoi(e) ? 1 : 0;
     if (const char* e = getenv("UINET_CKSUM_HOST_THREADS")) {
       const int v = atoi(e);
       if (v >= 1 && v <= 64) x.host_threads = v;
@@ -604,6 +605,8 @@ int uinet_cksum_set_tuning(const char* key, int value) {
     t.chains_tile = value;
   } else if (!strcmp(key, "xcd_remap") && (value == 0 || value == 1)) {
     t.xcd_remap = value;
+  } else if (!strcmp(key, "spans_lut") && (value == 0 || value == 1)) {
+    t.spans_lut = value;
   } else if (!strcmp(key, "host_threads") && value >= 1 && value <= 64) {
     t.host_threads = value;
   } else {

@@ -20,6 +20,7 @@ struct Tuning {
                        // wave-wide (0 = never)
   int chains_tile;     // flat chains: packets per wave tile, 0 = auto, 8, 32
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
+  int spans_lut;       // span kernels: LDS mask table + one's-complement sums (0/1)
 };
 const Tuning& tuning();
 

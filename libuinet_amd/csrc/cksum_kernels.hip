@@ -28,7 +28,7 @@
 namespace uinet {
 namespace {
 
-template <int G, int U, bool kStrided>
+template <int G, int U, bool kStrided, bool kLut>
 __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ base,
                                                  const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ len,
@@ -38,6 +38,8 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
                                                  uint16_t* __restrict__ out, uint32_t n,
                                                  uint32_t flags, uint32_t remap) {
   constexpr uint32_t kGroups = kBlock / G;
+  __shared__ MaskLut lut;
+  if (kLut) lut.init();  // before any early exit: it synchronises the block
   const int gl = threadIdx.x & (G - 1);
   const uint32_t stride = gridDim.x * kGroups;
   uint32_t p = logical_block(remap) * kGroups + threadIdx.x / G;
@@ -54,8 +56,14 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
     const uint32_t pc = min(pn, n - 1);
     const uint64_t on = kStrided ? (uint64_t)pc * pkt_stride : off[pc];
     const uint32_t ln = kStrided ? fixed_len : len[pc];
-    uint64_t acc = l ? sp.sum(0, gl) : 0;
-    if (sp.nch > (uint32_t)(G * U)) acc += sp.rest(gl);
+    uint64_t acc;
+    if (kLut) {
+      acc = l ? sp.sum_lut(lut, 0, gl) : 0;
+      if (sp.nch > (uint32_t)(G * U)) acc += sp.rest_lut(lut, gl);
+    } else {
+      acc = l ? sp.sum(0, gl) : 0;
+      if (sp.nch > (uint32_t)(G * U)) acc += sp.rest(gl);
+    }
     uint32_t x = fold16(acc);
     const uint32_t lp = parity ? parity[p] : 0u;
     if ((lp ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
@@ -121,10 +129,15 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = pick_geometry(len_hint);
   const int grid = grid_for(n, geo.g, 128);
-#define L(G, U)                                                                    \
-  hipLaunchKernelGGL((k_spans<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,  \
-                     static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, out, \
-                     n, flags, (uint32_t)tuning().xcd_remap)
+#define L(G, U)                                                                          \
+  if (tuning().spans_lut)                                                                \
+    hipLaunchKernelGGL((k_spans<G, U, false, true>), dim3(grid), dim3(kBlock), 0, stream, \
+                       static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
+                       out, n, flags, (uint32_t)tuning().xcd_remap);                     \
+  else                                                                                   \
+    hipLaunchKernelGGL((k_spans<G, U, false, false>), dim3(grid), dim3(kBlock), 0, stream, \
+                       static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
+                       out, n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
@@ -135,10 +148,15 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = pick_geometry(len);
   const int grid = grid_for(n, geo.g, 4096);
-#define L(G, U)                                                                     \
-  hipLaunchKernelGGL((k_spans<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,    \
-                     static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
-                     pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap)
+#define L(G, U)                                                                         \
+  if (tuning().spans_lut)                                                               \
+    hipLaunchKernelGGL((k_spans<G, U, true, true>), dim3(grid), dim3(kBlock), 0, stream, \
+                       static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
+                       pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap);    \
+  else                                                                                  \
+    hipLaunchKernelGGL((k_spans<G, U, true, false>), dim3(grid), dim3(kBlock), 0, stream, \
+                       static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
+                       pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
