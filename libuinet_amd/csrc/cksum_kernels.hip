@@ -113,9 +113,10 @@ int grid_for(uint32_t n, int g, int bpc) {
 
 }  // namespace
 
-// Blocks per CU.  Measured on MI355X (config 2, profiles/r01/sweep_grid): the
-// span kernel peaks at 64 (8 packets per group -- enough rounds for the
-// descriptor prefetch to pay, few enough that the tail is short); the
+// Blocks per CU.  Measured on MI355X by interleaved A/B (config 2,
+// profiles/r01/ab/): the span kernel peaks at 256 (2 packets per group --
+// the second packet's descriptors load under the first one's bytes; one
+// packet per group exposes the descriptor latency and loses 9 %); the
 // strided kernel has no descriptors and prefers one packet per group (no
 // cap).  UINET_CKSUM_BLOCKS_PER_CU overrides every kernel's default.
 int blocks_per_cu(int dflt) {
@@ -128,7 +129,7 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
                  uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = pick_geometry(len_hint);
-  const int grid = grid_for(n, geo.g, 128);
+  const int grid = grid_for(n, geo.g, 256);
 #define L(G, U)                                                                          \
   if (tuning().spans_lut)                                                                \
     hipLaunchKernelGGL((k_spans<G, U, false, true>), dim3(grid), dim3(kBlock), 0, stream, \
