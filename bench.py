@@ -38,8 +38,10 @@ CHAIN_CONFIGS = ("3", "3tx", "5tso")
 def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=200,
+                    help="untimed steps first: the first ~30-100 back-to-back launches run "
+                    "up to 25 %% slower while clocks settle (tools/drift.py)")
     ap.add_argument("--config", choices=["2", "2rx", "3", "3tx", "5", "5tso"], default="2",
                     help="BASELINE.json config shape (2 = the headline)")
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU")

@@ -56,7 +56,8 @@ static Tuning& tuning_rw() {
       const int v = atoi(e);
       x.blocks_per_cu = (v > 0 && v <= 4096) ? v : 0;
     }
-    if (const char* e = getenv("UINET_CKSUM_CHAINS")) x.chains_variant = e[0] == 's' ? 1 : 0;
+    if (const char* e = getenv("UINET_CKSUM_CHAINS")) x.chains_variant = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0'
+                                                       : e[0] == 's' ? 1 : e[0] == 'f' ? 2 : 0;
     if (const char* e = getenv("UINET_CKSUM_CHAINS_PASS")) {
       const int v = atoi(e);
       if (v == 2 || v == 4 || v == 8) x.chains_pass = v;
@@ -595,7 +596,7 @@ int uinet_cksum_set_tuning(const char* key, int value) {
   Tuning& t = tuning_rw();
   if (!strcmp(key, "blocks_per_cu") && value >= 0 && value <= 4096) {
     t.blocks_per_cu = value;
-  } else if (!strcmp(key, "chains_variant") && (value == 0 || value == 1)) {
+  } else if (!strcmp(key, "chains_variant") && value >= 0 && value <= 2) {
     t.chains_variant = value;
   } else if (!strcmp(key, "chains_pass") && (value == 2 || value == 4 || value == 8)) {
     t.chains_pass = value;

@@ -86,6 +86,19 @@ struct MaskLut {
   __device__ __forceinline__ uint64_t sum(u32x4 v, int s, int e) const {
     return masked_sum(v, m[clampi(s, 0, 16) * 17 + clampi(e, 0, 16)]);
   }
+  __device__ static __forceinline__ uint32_t index(int s, int e) {
+    return (uint32_t)(clampi(s, 0, 16) * 17 + clampi(e, 0, 16));
+  }
+  // sum_oc() of a precomputed index()
+  __device__ __forceinline__ uint32_t sum_oc_idx(u32x4 v, uint32_t i) const {
+    const u32x4 k = m[i];
+    unsigned c0, c1, c2, c3;
+    unsigned t = __builtin_addc(v.x & k.x, v.y & k.y, 0u, &c0);
+    t = __builtin_addc(t, v.z & k.z, c0, &c1);
+    t = __builtin_addc(t, v.w & k.w, c1, &c2);
+    t = __builtin_addc(t, 0u, c2, &c3);
+    return (t & 0xffff) + (t >> 16);
+  }
   // The same bytes as a 32-bit one's-complement sum (end-around carry) of
   // the masked words, folded once: < 2^17, congruent to sum() mod 65535
   // (2^32 - 1 = 65535 * 65537) and zero only when sum() is.  A carry out of

@@ -13,7 +13,7 @@ namespace uinet {
 // environment on first use.  0 = "use the kernel's default".
 struct Tuning {
   int blocks_per_cu;   // grid-stride width
-  int chains_variant;  // 0 flat, 1 serial
+  int chains_variant;  // 0 pipelined chunk stream, 1 serial, 2 unpipelined chunk stream
   int chains_pass;     // 2, 4, 8
   int host_threads;    // host-mbuf batch walk/pack threads, 1..64
   int chains_long;     // flat chains: segments of >= this many 16-B chunks stream

@@ -501,3 +501,77 @@ def test_chains_long_segments(torch_dev, ora, long_ch, tile):
     finally:
         u.set_tuning("chains_long", 128)
         u.set_tuning("chains_tile", 0)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_chains_kernel_variants(torch_dev, ora, variant):
+    """Every chain kernel variant (0 pipelined chunk stream, 1 serial walk,
+    2 unpipelined chunk stream) on chains of 0..150 segments with len/skip/seed
+    and the UDP flag."""
+    torch = torch_dev
+    rng = np.random.default_rng(8800 + variant)
+    arena = rand_arena(1 << 21, 47)
+    n = 1500
+    nseg = rng.integers(0, 151, n)
+    nseg[rng.random(n) < 0.1] = 0
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = np.where(rng.random(s) < 0.2, rng.integers(0, 4, s), rng.integers(1, 300, s))
+    seg_off = rng.integers(0, arena.size - 400, s).astype(np.int64)
+    tot = np.zeros(n, np.int64)
+    nz = nseg > 0
+    tot[nz] = np.add.reduceat(seg_len, pkt_seg[:-1][nz])
+    skip = (rng.random(n) * (tot + 1) * 0.3).astype(np.int64)
+    length = skip + (rng.random(n) * (tot - skip + 10)).astype(np.int64)
+    seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    u.set_tuning("chains_variant", variant)
+    try:
+        for flags in (0, u.F_UDP):
+            want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip,
+                              seed=seed, flags=flags)
+            got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off),
+                                 dev(torch, seg_len.astype(np.int32)),
+                                 dev(torch, pkt_seg.astype(np.int32)),
+                                 length=dev(torch, length.astype(np.int32)),
+                                 skip=dev(torch, skip.astype(np.int32)),
+                                 seed=dev(torch, seed.view(np.int32)), flags=flags, len_hint=120)
+            np.testing.assert_array_equal(host16(got), want)
+    finally:
+        u.set_tuning("chains_variant", 0)
+
+
+def test_chains_beyond_4gib_window(torch_dev, ora):
+    """A 4.5 GiB arena: even tiles keep their segments within 1 MiB of a tile
+    base anywhere in the arena (one 4 GiB window: 32-bit buffer offsets),
+    odd tiles scatter them over the whole arena (descriptor rounds that take
+    the 64-bit address path)."""
+    torch = torch_dev
+    size = (9 << 29) + 4096
+    d = torch.randint(0, 256, (size,), dtype=torch.uint8, device="cuda")
+    host = d.cpu().numpy()
+    rng = np.random.default_rng(4242)
+    n = 4096
+    nseg = rng.integers(1, 20, n)
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = rng.integers(0, 300, s)
+    pkt = np.repeat(np.arange(n), nseg)
+    tile_base = rng.integers(0, size - (2 << 20), n // 32 + 1)
+    local = tile_base[pkt // 32] + rng.integers(0, 1 << 20, s)
+    scattered = rng.integers(0, size - 512, s)
+    seg_off = np.where((pkt // 32) % 2 == 0, local, scattered).astype(np.int64)
+    seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    skip = np.full(n, 3, np.int64)
+    want = ora.chains(host, seg_off, seg_len, pkt_seg, skip=skip, seed=seed)
+    for variant in (0, 2):
+        u.set_tuning("chains_variant", variant)
+        try:
+            got = u.cksum_chains(d, dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
+                                 dev(torch, pkt_seg.astype(np.int32)),
+                                 skip=dev(torch, skip.astype(np.int32)),
+                                 seed=dev(torch, seed.view(np.int32)), len_hint=150)
+        finally:
+            u.set_tuning("chains_variant", 0)
+        np.testing.assert_array_equal(host16(got), want)
+    del d
+    torch.cuda.empty_cache()

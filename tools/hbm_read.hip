@@ -57,6 +57,33 @@ __global__ __launch_bounds__(256) void k_read_chunk(const uint4* __restrict__ p,
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+
+// Tile variant (the span kernel's access shape): logical tile t is 256 x U
+// consecutive 16-B chunks, one-shot or grid-stride over tiles; nt loads; with
+// `remap` block b takes logical id (b % 8) * (grid / 8) + b / 8 so each XCD
+// streams one contiguous band.
+template <int U, bool REMAP>
+__global__ __launch_bounds__(256) void k_read_tile(const uint4* __restrict__ p, uint64_t n16,
+                                                   uint32_t* __restrict__ sink) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t g = gridDim.x, per = g / 8;
+  uint32_t b = blockIdx.x;
+  if (REMAP && b < 8 * per) b = (b % 8) * per + b / 8;
+  const uint64_t tiles = (n16 + 256 * U - 1) / (256 * U);
+  uint32_t acc = 0;
+  for (uint64_t t = b; t < tiles; t += g) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = min(t * 256 * U + (uint64_t)u * 256 + threadIdx.x, n16 - 1);
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + i));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 template <typename F>
 float time_it(F f, int reps) {
   hipEvent_t a, b;
@@ -93,6 +120,19 @@ int main(int argc, char** argv) {
     report("stride_u4_nt", g, time_it([&] { k_read<4, true><<<g, 256>>>(p, n16, sink); }, 20));
     report("chunk_u4", g, time_it([&] { k_read_chunk<4><<<g, 256>>>(p, n16, sink); }, 20));
     report("chunk_u8", g, time_it([&] { k_read_chunk<8><<<g, 256>>>(p, n16, sink); }, 20));
+  }
+  {
+    const uint64_t t4 = (n16 + 1023) / 1024, t8 = (n16 + 2047) / 2048, t2 = (n16 + 511) / 512;
+    const int caps[] = {0, 256 * 64, 256 * 128, 256 * 256};
+    for (int cap : caps) {
+      auto G = [&](uint64_t t) { return (int)(cap && t > (uint64_t)cap ? cap : t); };
+      report(cap ? "tile_u2_gs" : "tile_u2", G(t2), time_it([&] { k_read_tile<2, false><<<G(t2), 256>>>(p, n16, sink); }, 20));
+      report(cap ? "tile_u4_gs" : "tile_u4", G(t4), time_it([&] { k_read_tile<4, false><<<G(t4), 256>>>(p, n16, sink); }, 20));
+      report(cap ? "tile_u8_gs" : "tile_u8", G(t8), time_it([&] { k_read_tile<8, false><<<G(t8), 256>>>(p, n16, sink); }, 20));
+      report(cap ? "tile_u2_xcd_gs" : "tile_u2_xcd", G(t2), time_it([&] { k_read_tile<2, true><<<G(t2), 256>>>(p, n16, sink); }, 20));
+      report(cap ? "tile_u4_xcd_gs" : "tile_u4_xcd", G(t4), time_it([&] { k_read_tile<4, true><<<G(t4), 256>>>(p, n16, sink); }, 20));
+      report(cap ? "tile_u8_xcd_gs" : "tile_u8_xcd", G(t8), time_it([&] { k_read_tile<8, true><<<G(t8), 256>>>(p, n16, sink); }, 20));
+    }
   }
   printf("]}\n");
   return 0;

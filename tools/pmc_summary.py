@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--key")
     ap.add_argument("--bytes", type=float, help="algorithmic bytes per dispatch")
     ap.add_argument("--out")
+    ap.add_argument("--last", type=int, default=100,
+                    help="also average the last N dispatches of each kernel (the bench's "
+                         "timed launches; the first ones are its untimed warmup)")
     a = ap.parse_args()
 
     res = {}
@@ -52,6 +55,15 @@ def main():
             res.setdefault(short(r["Name"]), {}).update(
                 calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), min_ns=float(r["MinNs"]),
                 max_ns=float(r["MaxNs"]))
+    trace = load_csv(a.prof_dir, "kernel_trace.csv")
+    durs = {}
+    for r in sorted(trace, key=lambda r: int(r["Start_Timestamp"])):
+        if a.kernel in r["Kernel_Name"]:
+            durs.setdefault(short(r["Kernel_Name"]), []).append(
+                int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for k, d in durs.items():
+        if k in res and a.last and len(d) > a.last:
+            res[k][f"avg_ns_last{a.last}"] = statistics.mean(d[-a.last:])
     pmc = load_csv(a.prof_dir, "counter_collection.csv")
     per = {}
     for r in pmc:

@@ -9,8 +9,8 @@ step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 "$secs" 
   echo "   rc=$rc"; grep -v "^[EW]20" "$OUT/$name.log" | tail -n 2
   case $rc in 0) ;; *) echo FATAL; exit $rc;; esac; }
 for c in ${CONFIGS:-2 3 3tx 5 5tso}; do
-  step bench_c$c 600 python3 bench.py --config $c --steps 20 --warmup 3 --cpu-baseline off
-  step trace_c$c 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_c$c" -o run --output-format csv -- python3 bench.py --config $c --steps 20 --warmup 3 --cpu-baseline off
+  step bench_c$c 600 python3 bench.py --config $c
+  step trace_c$c 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_c$c" -o run --output-format csv -- python3 bench.py --config $c --cpu-baseline off
   step pmc_c$c 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_c$c" -o run --output-format csv -- python3 bench.py --config $c --steps 10 --warmup 2 --cpu-baseline off
   read B N K <<<"$(python3 -c "import json; d=json.loads([l for l in open('$OUT/bench_c$c.log') if l.startswith('{')][-1]); print(d['config']['algorithmic_bytes_per_gpu'], d['config']['packets_per_gpu'], d['roofline']['kernel'])")"
   python3 tools/pmc_summary.py "$OUT/pmc_c$c" --key "$K:config$c:$N" --bytes "$B" --out profiles/pmc_traffic.json > "$OUT/pmc_c$c.summary.json"
