@@ -56,8 +56,9 @@ static Tuning& tuning_rw() {
       const int v = atoi(e);
       x.blocks_per_cu = (v > 0 && v <= 4096) ? v : 0;
     }
-    if (const char* e = getenv("UINET_CKSUM_CHAINS")) x.chains_variant = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0'
-                                                       : e[0] == 's' ? 1 : e[0] == 'f' ? 2 : 0;
+    if (const char* e = getenv("UINET_CKSUM_CHAINS"))
+      x.chains_variant = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0'
+                         : e[0] == 's' ? 1 : e[0] == 'f' ? 2 : 0;
     if (const char* e = getenv("UINET_CKSUM_CHAINS_PASS")) {
       const int v = atoi(e);
       if (v == 2 || v == 4 || v == 8) x.chains_pass = v;
@@ -302,6 +303,9 @@ struct Batch {
 thread_local Batch t_batch;
 
 constexpr int kChunkMin = 1024;  // packets; below this one thread walks
+// Staged batches up to this many bytes (descriptors + packed packet bytes) are
+// folded in place from mapped pinned memory instead of being copied to HBM.
+constexpr size_t kMappedStagingMax = 64 << 10;
 
 // Device address of [p, p + n) with a one-entry cache of the last region hit
 // (consecutive pieces almost always share a region).
@@ -469,17 +473,38 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
         cur += ((uint64_t)B.bytes[(size_t)i] + 15) & ~uint64_t(15);
       }
     });
-    rc = record_hip(hipMemcpyAsync(c.d_buf, c.h_buf, L.data_o + packed, hipMemcpyHostToDevice,
-                                   c.stream));
+    // A small batch (the per-call ABI is a batch of one) is folded straight
+    // out of the mapped staging and its results written straight back: one
+    // launch instead of copy + launch + copy, the two copies being most of
+    // its latency.  Large batches copy to HBM first (PCIe reads by the
+    // kernel are slower than one bulk DMA).
+    const bool mapped = L.data_o + packed <= kMappedStagingMax;
+    uint8_t* src = c.d_buf;
+    uint16_t* dout = c.d_out;
+    if (mapped) {
+      void* dd = nullptr;
+      void* dst = nullptr;
+      rc = record_hip(hipHostGetDevicePointer(&dd, c.h_buf, 0));
+      if (rc) return rc;
+      rc = record_hip(hipHostGetDevicePointer(&dst, c.h_out, 0));
+      if (rc) return rc;
+      src = static_cast<uint8_t*>(dd);
+      dout = static_cast<uint16_t*>(dst);
+    } else {
+      rc = record_hip(hipMemcpyAsync(c.d_buf, c.h_buf, L.data_o + packed,
+                                     hipMemcpyHostToDevice, c.stream));
+      if (rc) return rc;
+    }
+    rc = launch_spans(src + L.data_o, reinterpret_cast<const uint64_t*>(src + L.off_o),
+                      reinterpret_cast<const uint32_t*>(src + L.len_o),
+                      reinterpret_cast<const uint32_t*>(src + L.seed_o), src + L.par_o, dout,
+                      (uint32_t)n, flags, mean ? mean : 1, c.stream);
     if (rc) return rc;
-    rc = launch_spans(c.d_buf + L.data_o, reinterpret_cast<const uint64_t*>(c.d_buf + L.off_o),
-                      reinterpret_cast<const uint32_t*>(c.d_buf + L.len_o),
-                      reinterpret_cast<const uint32_t*>(c.d_buf + L.seed_o), c.d_buf + L.par_o,
-                      c.d_out, (uint32_t)n, flags, mean ? mean : 1, c.stream);
-    if (rc) return rc;
-    rc = record_hip(hipMemcpyAsync(c.h_out, c.d_out, (size_t)n * 2, hipMemcpyDeviceToHost,
-                                   c.stream));
-    if (rc) return rc;
+    if (!mapped) {
+      rc = record_hip(hipMemcpyAsync(c.h_out, c.d_out, (size_t)n * 2, hipMemcpyDeviceToHost,
+                                     c.stream));
+      if (rc) return rc;
+    }
   }
   rc = record_hip(hipStreamSynchronize(c.stream));
   if (rc) return rc;
