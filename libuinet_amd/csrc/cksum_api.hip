@@ -306,6 +306,8 @@ constexpr int kChunkMin = 1024;  // packets; below this one thread walks
 // Staged batches up to this many bytes (descriptors + packed packet bytes) are
 // folded in place from mapped pinned memory instead of being copied to HBM.
 constexpr size_t kMappedStagingMax = 64 << 10;
+// Staged batches of at least this many packet bytes overlap packing and copying.
+constexpr uint64_t kStreamCopyMin = 32ull << 20;
 
 // Device address of [p, p + n) with a one-entry cache of the last region hit
 // (consecutive pieces almost always share a region).
@@ -335,7 +337,9 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   if (rc) return rc;
 
   const int threads = tuning().host_threads;
-  int cs = (n + threads * 4 - 1) / (threads * 4);
+  // ~16 chunks per thread: the staging path packs and ships them in groups
+  // of `threads`, so packing group g+1 overlaps the copy of group g
+  int cs = (n + threads * 16 - 1) / (threads * 16);
   if (cs < kChunkMin) cs = kChunkMin;
   const int nch = (n + cs - 1) / cs;
   Batch& B = t_batch;
@@ -455,30 +459,45 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     uint32_t* seed = reinterpret_cast<uint32_t*>(c.h_buf + L.seed_o);
     uint8_t* par = c.h_buf + L.par_o;
     uint8_t* data = c.h_buf + L.data_o;
-    pool.run(nch, threads, [&](int j) {
-      const Chunk& C = B.chunks[(size_t)j];
-      uint64_t cur = C.pack_base;
-      uint32_t k = 0;
-      for (int i = C.i0; i < C.i1; i++) {
-        off[i] = cur;
-        seed[i] = B.seed[(size_t)i];
-        par[i] = B.par[(size_t)i];
-        len[i] = B.bytes[(size_t)i];
-        const uint32_t k1 = i + 1 < C.i1 ? B.pk_first[(size_t)i + 1] : (uint32_t)C.pieces.size();
-        uint8_t* dst = data + cur;
-        for (; k < k1; k++) {
-          memcpy(dst, C.pieces[k].p, C.pieces[k].n);
-          dst += C.pieces[k].n;
+    const bool mapped = L.data_o + packed <= kMappedStagingMax;
+    // A large batch is packed in groups of chunks, each group's bytes
+    // shipped to HBM (async DMA) while the pool packs the next group.
+    const bool stream_copy = !mapped && packed >= kStreamCopyMin;
+    const int group = stream_copy ? std::max(1, threads) : nch;
+    for (int g0 = 0; g0 < nch; g0 += group) {
+      const int g1 = std::min(nch, g0 + group);
+      pool.run(g1 - g0, threads, [&](int jj) {
+        const Chunk& C = B.chunks[(size_t)(g0 + jj)];
+        uint64_t cur = C.pack_base;
+        uint32_t k = 0;
+        for (int i = C.i0; i < C.i1; i++) {
+          off[i] = cur;
+          seed[i] = B.seed[(size_t)i];
+          par[i] = B.par[(size_t)i];
+          len[i] = B.bytes[(size_t)i];
+          const uint32_t k1 =
+              i + 1 < C.i1 ? B.pk_first[(size_t)i + 1] : (uint32_t)C.pieces.size();
+          uint8_t* dst = data + cur;
+          for (; k < k1; k++) {
+            memcpy(dst, C.pieces[k].p, C.pieces[k].n);
+            dst += C.pieces[k].n;
+          }
+          cur += ((uint64_t)B.bytes[(size_t)i] + 15) & ~uint64_t(15);
         }
-        cur += ((uint64_t)B.bytes[(size_t)i] + 15) & ~uint64_t(15);
+      });
+      if (stream_copy) {
+        const uint64_t b0 = B.chunks[(size_t)g0].pack_base;
+        const uint64_t b1 = g1 < nch ? B.chunks[(size_t)g1].pack_base : packed;
+        rc = record_hip(hipMemcpyAsync(c.d_buf + L.data_o + b0, data + b0, b1 - b0,
+                                       hipMemcpyHostToDevice, c.stream));
+        if (rc) return rc;
       }
-    });
+    }
     // A small batch (the per-call ABI is a batch of one) is folded straight
     // out of the mapped staging and its results written straight back: one
     // launch instead of copy + launch + copy, the two copies being most of
     // its latency.  Large batches copy to HBM first (PCIe reads by the
     // kernel are slower than one bulk DMA).
-    const bool mapped = L.data_o + packed <= kMappedStagingMax;
     uint8_t* src = c.d_buf;
     uint16_t* dout = c.d_out;
     if (mapped) {
@@ -491,7 +510,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
       src = static_cast<uint8_t*>(dd);
       dout = static_cast<uint16_t*>(dst);
     } else {
-      rc = record_hip(hipMemcpyAsync(c.d_buf, c.h_buf, L.data_o + packed,
+      rc = record_hip(hipMemcpyAsync(c.d_buf, c.h_buf, stream_copy ? L.data_o : L.data_o + packed,
                                      hipMemcpyHostToDevice, c.stream));
       if (rc) return rc;
     }

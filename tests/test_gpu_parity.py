@@ -575,3 +575,28 @@ def test_chains_beyond_4gib_window(torch_dev, ora):
         np.testing.assert_array_equal(host16(got), want)
     del d
     torch.cuda.empty_cache()
+
+
+def test_host_batch_stream_copy(torch_dev, ora):
+    """A staged host batch large enough (>= 32 MiB of packet bytes) to be
+    packed and shipped to HBM in overlapped groups; chained and odd-offset
+    packets included, so every group boundary lands mid-layout."""
+    rng = np.random.default_rng(77)
+    n = 64000  # ~45 MB of summed bytes
+    arena = rand_arena(1500 * n + 8192, 77)
+    lens = rng.choice([64, 576, 1500], n)
+    off = (np.arange(n) * 1500 + rng.integers(0, 7, n)).astype(np.int64)
+    ch = MbufChains.contiguous(arena, off, lens)
+    skip = rng.integers(0, 30, n).astype(np.int32)
+    want = ora.skip_batch(ch.heads, lens, skip)
+    np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, lens, skip), want)
+    # chained: every packet re-cut into 1..256-B segments
+    seg_off, seg_len, pkt_seg = [], [], [0]
+    for i in range(n):
+        cuts = np.cumsum(rng.integers(1, 257, 12))
+        cuts = np.concatenate([[0], cuts[cuts < lens[i]], [lens[i]]])
+        seg_off.extend(off[i] + cuts[:-1])
+        seg_len.extend(np.diff(cuts))
+        pkt_seg.append(len(seg_off))
+    cc = MbufChains(arena, np.array(seg_off), np.array(seg_len), np.array(pkt_seg))
+    np.testing.assert_array_equal(u.in_cksum_skip_batch(cc.heads, lens, skip), want)
