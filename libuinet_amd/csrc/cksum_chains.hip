@@ -94,7 +94,9 @@ __global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restric
                                                        const uint32_t* __restrict__ seed,
                                                        uint16_t* __restrict__ out, uint32_t n,
                                                        uint32_t flags, uint32_t long_ch) {
-  static_assert(kTile >= 1 && kTile <= 64, "a tile's packets are one per lane");
+  static_assert(kTile >= 1 && kTile <= 32,
+                "a tile's packets are one per lane, lane kTile reads the end of its segment "
+                "range, and its 2 * kTile bins are one per lane");
   constexpr int kWin = 64 * kPass;  // chunks per batch of passes
   __shared__ MaskLut lut;
   // per packet two sums: bytes at even / odd logical-vs-address parity
@@ -337,7 +339,9 @@ __global__ __launch_bounds__(kBlock) void k_chains_pipe(const uint8_t* __restric
                                                        const uint32_t* __restrict__ seed,
                                                        uint16_t* __restrict__ out, uint32_t n,
                                                        uint32_t flags, uint32_t long_ch) {
-  static_assert(kTile >= 1 && kTile <= 64, "a tile's packets are one per lane");
+  static_assert(kTile >= 1 && kTile <= 32,
+                "a tile's packets are one per lane, lane kTile reads the end of its segment "
+                "range, and its 2 * kTile bins are one per lane");
   constexpr int kWin = 64 * kPass;  // chunks per batch of passes
   __shared__ MaskLut lut;
   __shared__ unsigned long long lds_acc[kWaves][2 * kTile];  // (slot, rot) bins
