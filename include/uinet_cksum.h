@@ -134,7 +134,7 @@ int uinet_cksum_device_ok(void);
  *   "spans_lut"       span kernels: LDS mask table + one's-complement chunk
  *                     sums (1, default) or register masks + 64-bit sums (0)
  *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
- *                     1..64 (default min(8, hardware threads))
+ *                     1..64 (default min(16, hardware threads))
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
  * (0|1|2, or serial|flat), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,

@@ -51,7 +51,7 @@ int check_launch() { return record_hip(hipGetLastError()); }
 static Tuning& tuning_rw() {
   static Tuning t = [] {
     const unsigned hw = std::thread::hardware_concurrency();
-    Tuning x{0, 0, 2, (int)std::min(8u, hw ? hw : 1u), 128, 0, 1, 1};
+    Tuning x{0, 0, 2, (int)std::min(16u, hw ? hw : 1u), 128, 0, 1, 1};
     if (const char* e = getenv("UINET_CKSUM_BLOCKS_PER_CU")) {
       const int v = atoi(e);
       x.blocks_per_cu = (v > 0 && v <= 4096) ? v : 0;

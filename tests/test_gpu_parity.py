@@ -464,7 +464,7 @@ def test_host_batch_chunked(torch_dev, ora, host_threads):
         finally:
             u.unregister_host(arena)
     finally:
-        u.set_tuning("host_threads", 8)
+        u.set_tuning("host_threads", 16)
 
 
 @pytest.mark.parametrize("long_ch,tile", [(0, 32), (16, 8), (16, 32), (64, 0), (200, 8)])
