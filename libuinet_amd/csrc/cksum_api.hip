@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -48,41 +49,75 @@ int record_hip(hipError_t e) {
 
 int check_launch() { return record_hip(hipGetLastError()); }
 
-static Tuning& tuning_rw() {
-  static Tuning t = [] {
+// The live knob values.  uinet_cksum_set_tuning may run while other threads
+// launch, so each knob is a relaxed atomic and a launch reads one snapshot
+// (tuning()).  The environment seeds them through the same validation.
+struct TuningLive {
+  std::atomic<int> blocks_per_cu{0}, chains_variant{0}, chains_pass{2}, host_threads{8},
+      chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1};
+};
+
+static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
+  struct Knob {
+    const char* key;
+    std::atomic<int> TuningLive::*field;
+    bool (*ok)(int);
+  };
+  static const Knob knobs[] = {
+      {"blocks_per_cu", &TuningLive::blocks_per_cu, [](int v) { return v >= 0 && v <= 4096; }},
+      {"chains_variant", &TuningLive::chains_variant, [](int v) { return v >= 0 && v <= 2; }},
+      {"chains_pass", &TuningLive::chains_pass, [](int v) { return v == 2 || v == 4 || v == 8; }},
+      {"chains_long", &TuningLive::chains_long,
+       [](int v) { return v == 0 || (v >= 16 && v <= (1 << 24)); }},
+      {"chains_tile", &TuningLive::chains_tile,
+       [](int v) { return v == 0 || v == 8 || v == 32; }},
+      {"xcd_remap", &TuningLive::xcd_remap, [](int v) { return v == 0 || v == 1; }},
+      {"spans_lut", &TuningLive::spans_lut, [](int v) { return v == 0 || v == 1; }},
+      {"host_threads", &TuningLive::host_threads, [](int v) { return v >= 1 && v <= 64; }},
+  };
+  for (const Knob& k : knobs)
+    if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
+  return nullptr;
+}
+
+static TuningLive& tuning_live() {
+  static TuningLive* t = [] {
+    auto* x = new TuningLive;  // never freed: launches may run during exit
     const unsigned hw = std::thread::hardware_concurrency();
-    Tuning x{0, 0, 2, (int)std::min(16u, hw ? hw : 1u), 128, 0, 1, 1};
-    if (const char* e = getenv("UINET_CKSUM_BLOCKS_PER_CU")) {
-      const int v = atoi(e);
-      x.blocks_per_cu = (v > 0 && v <= 4096) ? v : 0;
-    }
-    if (const char* e = getenv("UINET_CKSUM_CHAINS"))
-      x.chains_variant = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0'
-                         : e[0] == 's' ? 1 : e[0] == 'f' ? 2 : 0;
-    if (const char* e = getenv("UINET_CKSUM_CHAINS_PASS")) {
-      const int v = atoi(e);
-      if (v == 2 || v == 4 || v == 8) x.chains_pass = v;
-    }
-    if (const char* e = getenv("UINET_CKSUM_CHAINS_LONG")) {
-      const int v = atoi(e);
-      if (v == 0 || (v >= 16 && v <= (1 << 24))) x.chains_long = v;
-    }
-    if (const char* e = getenv("UINET_CKSUM_CHAINS_TILE")) {
-      const int v = atoi(e);
-      if (v == 0 || v == 8 || v == 32) x.chains_tile = v;
-    }
-    if (const char* e = getenv("UINET_CKSUM_XCD_REMAP")) x.xcd_remap = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("UINET_CKSUM_SPANS_LUT")) x.spans_lut = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("UINET_CKSUM_HOST_THREADS")) {
-      const int v = atoi(e);
-      if (v >= 1 && v <= 64) x.host_threads = v;
+    x->host_threads = (int)std::min(16u, hw ? hw : 1u);
+    static const char* const env[][2] = {
+        {"UINET_CKSUM_BLOCKS_PER_CU", "blocks_per_cu"}, {"UINET_CKSUM_CHAINS", "chains_variant"},
+        {"UINET_CKSUM_CHAINS_PASS", "chains_pass"},     {"UINET_CKSUM_CHAINS_LONG", "chains_long"},
+        {"UINET_CKSUM_CHAINS_TILE", "chains_tile"},     {"UINET_CKSUM_XCD_REMAP", "xcd_remap"},
+        {"UINET_CKSUM_SPANS_LUT", "spans_lut"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
+    };
+    for (const auto& kv : env) {
+      const char* e = getenv(kv[0]);
+      if (!e || !*e) continue;
+      int v = atoi(e);
+      if (!strcmp(kv[1], "chains_variant") && (e[0] == 's' || e[0] == 'f')) v = e[0] == 's' ? 1 : 2;
+      if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_lut")) v = v ? 1 : 0;
+      if (std::atomic<int>* f = tuning_field(*x, kv[1], v)) f->store(v, std::memory_order_relaxed);
     }
     return x;
   }();
-  return t;
+  return *t;
 }
 
-const Tuning& tuning() { return tuning_rw(); }
+Tuning tuning() {
+  const TuningLive& t = tuning_live();
+  const auto ld = [](const std::atomic<int>& a) { return a.load(std::memory_order_relaxed); };
+  Tuning x;
+  x.blocks_per_cu = ld(t.blocks_per_cu);
+  x.chains_variant = ld(t.chains_variant);
+  x.chains_pass = ld(t.chains_pass);
+  x.host_threads = ld(t.host_threads);
+  x.chains_long = ld(t.chains_long);
+  x.chains_tile = ld(t.chains_tile);
+  x.xcd_remap = ld(t.xcd_remap);
+  x.spans_lut = ld(t.spans_lut);
+  return x;
+}
 
 namespace {
 
@@ -637,26 +672,9 @@ int uinet_cksum_unregister_host(void* base) {
 
 int uinet_cksum_set_tuning(const char* key, int value) {
   if (!key) return UINET_CKSUM_EINVAL;
-  Tuning& t = tuning_rw();
-  if (!strcmp(key, "blocks_per_cu") && value >= 0 && value <= 4096) {
-    t.blocks_per_cu = value;
-  } else if (!strcmp(key, "chains_variant") && value >= 0 && value <= 2) {
-    t.chains_variant = value;
-  } else if (!strcmp(key, "chains_pass") && (value == 2 || value == 4 || value == 8)) {
-    t.chains_pass = value;
-  } else if (!strcmp(key, "chains_long") && (value == 0 || (value >= 16 && value <= (1 << 24)))) {
-    t.chains_long = value;
-  } else if (!strcmp(key, "chains_tile") && (value == 0 || value == 8 || value == 32)) {
-    t.chains_tile = value;
-  } else if (!strcmp(key, "xcd_remap") && (value == 0 || value == 1)) {
-    t.xcd_remap = value;
-  } else if (!strcmp(key, "spans_lut") && (value == 0 || value == 1)) {
-    t.spans_lut = value;
-  } else if (!strcmp(key, "host_threads") && value >= 1 && value <= 64) {
-    t.host_threads = value;
-  } else {
-    return UINET_CKSUM_EINVAL;
-  }
+  std::atomic<int>* f = tuning_field(tuning_live(), key, value);
+  if (!f) return UINET_CKSUM_EINVAL;
+  f->store(value, std::memory_order_relaxed);
   return UINET_CKSUM_OK;
 }
 

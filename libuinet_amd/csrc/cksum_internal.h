@@ -10,7 +10,8 @@
 namespace uinet {
 
 // Process-wide performance knobs (uinet_cksum_set_tuning); seeded from the
-// environment on first use.  0 = "use the kernel's default".
+// environment on first use.  0 = "use the kernel's default".  tuning() returns
+// a snapshot of the live values (relaxed atomics in cksum_api.hip).
 struct Tuning {
   int blocks_per_cu;   // grid-stride width
   int chains_variant;  // 0 pipelined chunk stream, 1 serial, 2 unpipelined chunk stream
@@ -22,7 +23,7 @@ struct Tuning {
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
   int spans_lut;       // span kernels: LDS mask table + one's-complement sums (0/1)
 };
-const Tuning& tuning();
+Tuning tuning();
 
 // Records the HIP error (if any) of the last launch on this thread and maps
 // it to a UINET_CKSUM_* code.

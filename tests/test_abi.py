@@ -67,21 +67,66 @@ def test_fold_helpers_match_reference(golden):
         assert u.in_addword(int(a), int(b)) == e
 
 
-def test_in_cksum_update_inline():
-    """The header's uinet_in_cksum_update == in_cksum.h:55-61 on raw bytes."""
+def _ip_fold(h: bytes) -> int:
+    s = sum(int.from_bytes(h[k:k + 2], "big") for k in range(0, len(h), 2))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+def test_in_cksum_update_inline(tmp_path):
+    """The header's static inline uinet_in_cksum_update, compiled by gcc from
+    include/uinet_cksum.h, against in_cksum.h:55-61 (ntohs(ip_sum) + 256,
+    end-around carry, htons) on every ip_sum value, and as the forwarding
+    path uses it: after ip_ttl -= 1 the header still verifies."""
     import ctypes
 
-    # compile-free check: restate the reference formula in Python
-    for s in (0, 1, 0xFEFF, 0xFF00, 0xFFFF, 0x1234):
+    src = tmp_path / "upd.c"
+    src.write_text('#include "uinet_cksum.h"\nvoid upd(void *h) { uinet_in_cksum_update(h); }\n')
+    so = tmp_path / "upd.so"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-shared", "-fPIC",
+                    "-I", os.path.join(REPO, "include"), "-o", str(so), str(src)], check=True)
+    upd = ctypes.CDLL(str(so)).upd
+    upd.argtypes = [ctypes.c_void_p]
+    buf = (ctypes.c_uint8 * 20)()
+    for s in range(0x10000):  # every ip_sum
+        buf[10], buf[11] = s >> 8, s & 0xFF
+        upd(buf)
         t = s + 256
-        want = (t + (t >> 16)) & 0xFFFF
-        hdr = bytearray(20)
-        hdr[10:12] = s.to_bytes(2, "big")
-        # mirror of the static inline in include/uinet_cksum.h
-        v = int.from_bytes(hdr[10:12], "big") + 256
-        v = v + (v >> 16)
-        assert v & 0xFFFF == want
-    assert ctypes.sizeof(ctypes.c_uint16) == 2
+        assert (buf[10] << 8 | buf[11]) == (t + (t >> 16)) & 0xFFFF, s
+    rng = np.random.default_rng(11)
+    for _ in range(2000):
+        h = bytearray(rng.integers(0, 256, 20, dtype=np.uint8).tobytes())
+        h[8] = int(rng.integers(1, 256))  # ttl >= 1
+        h[10:12] = b"\0\0"
+        h[10:12] = (~_ip_fold(h) & 0xFFFF).to_bytes(2, "big")
+        assert _ip_fold(h) == 0xFFFF
+        h[8] -= 1  # ip_fastfwd.c: ip->ip_ttl -= IPTTLDEC, then in_cksum_update(ip)
+        ctypes.memmove(buf, bytes(h), 20)
+        upd(buf)
+        assert _ip_fold(bytes(buf)) == 0xFFFF
+
+
+def test_set_tuning_validation():
+    """uinet_cksum_set_tuning accepts each documented knob's range and rejects
+    unknown keys and out-of-range values (no device needed)."""
+    L = u.lib()
+    ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_variant", 2),
+          ("chains_pass", 4), ("chains_long", 0), ("chains_long", 16), ("chains_tile", 8),
+          ("xcd_remap", 0), ("spans_lut", 1), ("host_threads", 64)]
+    bad = [("blocks_per_cu", -1), ("chains_variant", 3), ("chains_pass", 3), ("chains_long", 15),
+           ("chains_tile", 64), ("xcd_remap", 2), ("host_threads", 0), ("no_such_knob", 1)]
+    try:
+        for k, v in ok:
+            assert L.uinet_cksum_set_tuning(k.encode(), v) == 0, (k, v)
+        for k, v in bad:
+            assert L.uinet_cksum_set_tuning(k.encode(), v) == u.EINVAL, (k, v)
+        assert L.uinet_cksum_set_tuning(None, 1) == u.EINVAL
+    finally:  # back to the defaults
+        for k, v in [("blocks_per_cu", 0), ("chains_variant", 0), ("chains_pass", 2),
+                     ("chains_long", 128), ("chains_tile", 0), ("xcd_remap", 1), ("spans_lut", 1),
+                     ("host_threads", min(16, os.cpu_count() or 1))]:
+            L.uinet_cksum_set_tuning(k.encode(), v)
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")
