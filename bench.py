@@ -42,8 +42,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=200,
                     help="untimed steps first: the first ~30-100 back-to-back launches run "
                     "up to 25 %% slower while clocks settle (tools/drift.py)")
-    ap.add_argument("--config", choices=["2", "2rx", "3", "3tx", "5", "5tso"], default="2",
-                    help="BASELINE.json config shape (2 = the headline)")
+    ap.add_argument("--config", choices=["2", "2rx", "2s", "3", "3tx", "5", "5tso"], default="2",
+                    help="BASELINE.json config shape (2 = the headline; 2s = 16 M x 64 B "
+                    "packets, a small-packet shape outside BASELINE.json)")
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU")
     ap.add_argument("--api", choices=["spans", "strided"], default="spans")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -73,6 +74,12 @@ def build_workload(cfg: str, n, rank: int):
         w["desc"] = (f"config{cfg}: {n:,} x 1500 B contiguous packets (stride {w['stride']}"
                      f"{', +14' if cfg == '2rx' else ''}), device-resident, in_cksum_skip(m,1500,0)")
         w["hint"] = 1500
+    elif cfg == "2s":
+        n = n or (1 << 24)
+        w = W.config2_device(n, stride=64, length=64, rank=rank)
+        w["desc"] = (f"config2s: {n:,} x 64 B contiguous packets (stride 64), device-resident, "
+                     f"in_cksum_skip(m,64,0) -- small-packet shape, not a BASELINE.json config")
+        w["hint"] = 64
     elif cfg == "3":
         n = n or (1 << 20)
         w = W.config3_device(n, rank=rank)
@@ -107,7 +114,7 @@ def make_launch(cfg: str, w, api: str, out):
         return lambda s: u.cksum_chains(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"],
                                         length=w["len"], skip=w["skip"], seed=w.get("seed"),
                                         out=out, len_hint=w["hint"], stream=s)
-    if api == "strided" and cfg in ("2", "2rx"):
+    if api == "strided" and cfg in ("2", "2rx", "2s"):
         base = w["arena"][w["base"]:]
         return lambda s: u.cksum_strided(base, w["stride"], w["length"], w["n"], out=out, stream=s)
     seed = w.get("seed")
@@ -290,6 +297,7 @@ def main():
             "steps": K,
             "warmup": Wm,
             "ms_per_step": round(elapsed / K * 1e3, 4),
+            "packets_per_s": round(n * world * K / elapsed, 1),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

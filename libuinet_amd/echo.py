@@ -23,7 +23,7 @@ cluster at +14 (uinet_if_netmap.c:1504-1523):
 
 `engine` is anything with skip_batch / hdr_batch / pseudo_header_batch over
 mbuf heads (the GPU engine adapter below, or the oracle / reference objects
-used by the tests and tools/echo_replay.py).
+used by the tests and tests/perf/echo_replay.py).
 """
 from __future__ import annotations
 

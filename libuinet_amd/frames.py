@@ -1,6 +1,6 @@
 """Synthetic Ethernet/IPv4 frame batches for the driver offload hooks
 (``uinet_cksum_rx_offload`` / ``uinet_cksum_tx_offload``): tests and
-tools/offload_rate.py.
+tests/perf/offload_rate.py.
 
 A TX batch is laid out the way tcp_output / udp_output hand packets to the
 driver when the interface advertises checksum offload: a header mbuf holding

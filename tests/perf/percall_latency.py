@@ -3,7 +3,7 @@
 batches of various sizes, vs the reference object on the same host mbufs."""
 import json, os, sys, time
 import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: F401  (one HIP runtime)
 import libuinet_amd as u
 import oracle

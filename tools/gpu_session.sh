@@ -38,8 +38,8 @@ if [[ $WHAT == all || $WHAT == variants || $WHAT == tests+variants ]]; then
   run prof_variants_tso 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_variants_tso" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --config 5tso --cpu-baseline off
 fi
 if [[ $WHAT == all || $WHAT == host || $WHAT == tests+host ]]; then
-  run echo_replay 600 python tools/echo_replay.py
-  run host_path 600 python tools/host_path.py
-  run offload_rate 600 python tools/offload_rate.py
+  run echo_replay 600 python tests/perf/echo_replay.py
+  run host_path 600 python tests/perf/host_path.py
+  run offload_rate 600 python tests/perf/offload_rate.py
 fi
 echo "== done"

@@ -1,6 +1,6 @@
 set -u
 OUT=gpurun_out/r01q; mkdir -p $OUT
-UINET_CKSUM_HOST_THREADS=16 timeout -k 10 600 python tools/host_path.py > $OUT/host_path_t16.log 2>&1 || exit $?
+UINET_CKSUM_HOST_THREADS=16 timeout -k 10 600 python tests/perf/host_path.py > $OUT/host_path_t16.log 2>&1 || exit $?
 tail -1 $OUT/host_path_t16.log
 bash tools/pmc_sets.sh r01q/sq_c2 --config 2 || exit $?
 python3 tools/pmc_table.py gpurun_out/r01q/sq_c2 > gpurun_out/r01q/sq_c2/summary.txt
