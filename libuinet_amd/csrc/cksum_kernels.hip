@@ -85,6 +85,7 @@ struct Geometry {
 // lanes x 3 loads = 96 chunks >= the 95 a 1500-B span can touch).
 Geometry pick_geometry(uint32_t mean_len) {
   if (mean_len == 0) return {64, 2};
+  if (mean_len <= 64) return {4, 2};  // 16 packets per wave; an unaligned 64-B span spans 5 chunks
   if (mean_len <= 96) return {8, 1};
   if (mean_len <= 224) return {8, 2};
   if (mean_len <= 720) return {16, 3};
@@ -103,6 +104,7 @@ int grid_for(uint32_t n, int g, int bpc) {
 
 #define UINET_DISPATCH_GEOMETRY(GEO, LAUNCH)          \
   switch ((GEO).g * 16 + (GEO).u) {                   \
+    case 4 * 16 + 2: LAUNCH(4, 2); break;             \
     case 8 * 16 + 1: LAUNCH(8, 1); break;             \
     case 8 * 16 + 2: LAUNCH(8, 2); break;             \
     case 16 * 16 + 3: LAUNCH(16, 3); break;           \
