@@ -600,3 +600,56 @@ def test_host_batch_stream_copy(torch_dev, ora):
         pkt_seg.append(len(seg_off))
     cc = MbufChains(arena, np.array(seg_off), np.array(seg_len), np.array(pkt_seg))
     np.testing.assert_array_equal(u.in_cksum_skip_batch(cc.heads, lens, skip), want)
+
+
+def test_device_api_on_side_streams(torch_dev, ora):
+    """The device-resident entry points enqueue on the caller's stream: four
+    side streams with a span, a strided, a chain and a seeded span batch in
+    flight together, then four host threads each looping on its own stream."""
+    torch = torch_dev
+    rng = np.random.default_rng(606)
+    arena = rand_arena(1 << 22, 66)
+    d = dev(torch, arena)
+    n = 20000
+    off = rng.integers(0, arena.size - 3000, n)
+    ln = rng.integers(0, 2000, n)
+    seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    seg_off, seg_len, pkt_seg = random_chain_layout(rng, 3000, arena.size)
+    want = [ora.spans(arena, off, ln), ora.spans(arena, 1514 * np.arange(2000) + 14, 1500),
+            ora.chains(arena, seg_off, seg_len, pkt_seg), ora.spans(arena, off, ln, seed)]
+    t_off, t_ln, t_seed = dev(torch, off), dev(torch, ln.astype(np.int32)), dev(torch, seed.view(np.int32))
+    t_so, t_sl = dev(torch, seg_off), dev(torch, seg_len.astype(np.int32))
+    t_ps = dev(torch, pkt_seg.astype(np.int32))
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    outs = [torch.empty(w.size, dtype=torch.uint16, device="cuda") for w in want]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        u.cksum_spans(d, t_off, t_ln, out=outs[0], stream=streams[0])
+        u.cksum_strided(d[14:], 1514, 1500, 2000, out=outs[1], stream=streams[1])
+        u.cksum_chains(d, t_so, t_sl, t_ps, out=outs[2], stream=streams[2])
+        u.cksum_spans(d, t_off, t_ln, seed=t_seed, out=outs[3], stream=streams[3])
+    torch.cuda.synchronize()
+    for o, w in zip(outs, want):
+        np.testing.assert_array_equal(host16(o), w)
+
+    errors, got = [], {}
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream()
+            o = torch.empty(n, dtype=torch.uint16, device="cuda")
+            for _ in range(5):
+                u.cksum_spans(d, t_off, t_ln, seed=t_seed if k % 2 else None, out=o, stream=s)
+            s.synchronize()
+            got[k] = host16(o)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+    for k in range(4):
+        np.testing.assert_array_equal(got[k], want[3] if k % 2 else want[0])
