@@ -39,18 +39,24 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
                                                  uint32_t flags, uint32_t remap) {
   constexpr uint32_t kGroups = kBlock / G;
   __shared__ MaskLut lut;
-  if (kLut) lut.init();  // before any early exit: it synchronises the block
   const int gl = threadIdx.x & (G - 1);
   const uint32_t stride = gridDim.x * kGroups;
   uint32_t p = logical_block(remap) * kGroups + threadIdx.x / G;
-  if (p >= n) return;  // whole groups leave together
-  uint64_t o = kStrided ? (uint64_t)p * pkt_stride : off[p];
-  uint32_t l = kStrided ? fixed_len : len[p];
+  const bool live = p < n;
+  uint64_t o = 0;
+  uint32_t l = 0;
+  if (live) {
+    o = kStrided ? (uint64_t)p * pkt_stride : off[p];
+    l = kStrided ? fixed_len : len[p];
+  }
+  const uint8_t* a = base + o;
+  Span<G, U> sp;
+  sp.init(a, l);
+  if (l) sp.load(0, gl);  // the first packet's bytes are in flight ...
+  if (kLut) lut.init();   // ... while the block fills its mask table (every thread
+                          // reaches this barrier: no exit before it)
+  if (!live) return;      // whole groups leave together
   for (;;) {
-    const uint8_t* a = base + o;
-    Span<G, U> sp;
-    sp.init(a, l);
-    if (l) sp.load(0, gl);
     // prefetch the next packet's descriptors behind this packet's loads
     const uint32_t pn = p + stride;
     const uint32_t pc = min(pn, n - 1);
@@ -73,6 +79,9 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
     p = pn;
     o = on;
     l = ln;
+    a = base + o;
+    sp.init(a, l);
+    if (l) sp.load(0, gl);
   }
 }
 
