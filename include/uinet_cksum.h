@@ -149,8 +149,13 @@ int uinet_cksum_set_tuning(const char *key, int value);
 /* All array pointers are device pointers (HBM).  Launches are asynchronous  */
 /* on `stream` (a hipStream_t; NULL = the legacy default stream).  A         */
 /* `len_hint` (mean bytes per packet, 0 = unknown) selects the lanes-per-    */
-/* packet geometry; it never changes results.                                */
+/* packet geometry; it never changes results.  A launch takes at most        */
+/* UINET_CKSUM_MAX_PACKETS packets (more: UINET_CKSUM_EINVAL) and, for       */
+/* chains, fewer than 2^31 segments; descriptors must point at device bytes  */
+/* the kernel may read (the checksum, like the reference, trusts its input). */
 /* ------------------------------------------------------------------------ */
+
+#define UINET_CKSUM_MAX_PACKETS 0x80000000u
 
 /* One contiguous span per packet:
  *   out[i] = checksum of bytes [base + off[i], base + off[i] + len[i])

@@ -693,6 +693,7 @@ int uinet_cksum_spans(const void* base, const uint64_t* off, const uint32_t* len
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, uint32_t len_hint, void* stream) {
   if (n == 0) return UINET_CKSUM_OK;
+  if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
   if (!base || !off || !len || !out) return UINET_CKSUM_EINVAL;
   return launch_spans(base, off, len, seed, parity, out, n, flags, len_hint,
                       static_cast<hipStream_t>(stream));
@@ -701,6 +702,7 @@ int uinet_cksum_spans(const void* base, const uint64_t* off, const uint32_t* len
 int uinet_cksum_strided(const void* base, uint64_t stride, uint32_t len, const uint32_t* seed,
                         uint16_t* out, uint32_t n, uint32_t flags, void* stream) {
   if (n == 0) return UINET_CKSUM_OK;
+  if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
   if (!base || !out) return UINET_CKSUM_EINVAL;
   return launch_strided(base, stride, len, seed, out, n, flags,
                         static_cast<hipStream_t>(stream));
@@ -711,6 +713,7 @@ int uinet_cksum_chains(const void* base, const uint64_t* seg_off, const uint32_t
                        const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
                        uint32_t len_hint, void* stream) {
   if (n == 0) return UINET_CKSUM_OK;
+  if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
   if (!base || !seg_off || !seg_len || !pkt_seg || !out) return UINET_CKSUM_EINVAL;
   return launch_chains(base, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags,
                        len_hint, static_cast<hipStream_t>(stream));

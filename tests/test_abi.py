@@ -139,3 +139,17 @@ def test_no_silent_cpu_fallback():
     with pytest.raises(u.CksumError):
         u.in_cksum_hdr_batch(np.array([a.ctypes.data], np.uint64))
     assert u.lib().uinet_cksum_device_ok() == 0
+
+
+def test_device_api_rejects_oversized_launch():
+    """More than UINET_CKSUM_MAX_PACKETS packets in one launch is EINVAL,
+    decided before anything touches a device; n == 0 is a no-op."""
+    L = u.lib()
+    p = 16  # never dereferenced: both checks come first
+    big = 0x80000001
+    assert L.uinet_cksum_spans(p, p, p, None, None, p, big, 0, 0, None) == u.EINVAL
+    assert L.uinet_cksum_strided(p, 1500, 1500, None, p, big, 0, None) == u.EINVAL
+    assert L.uinet_cksum_chains(p, p, p, p, None, None, None, p, big, 0, 0, None) == u.EINVAL
+    assert L.uinet_cksum_spans(p, p, p, None, None, p, 0, 0, 0, None) == 0
+    text = open(HEADER).read()
+    assert "#define UINET_CKSUM_MAX_PACKETS 0x80000000u" in text

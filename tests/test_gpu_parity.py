@@ -573,6 +573,14 @@ def test_chains_beyond_4gib_window(torch_dev, ora):
         finally:
             u.set_tuning("chains_variant", 0)
         np.testing.assert_array_equal(host16(got), want)
+    # spans and strided packets past the 4 GiB mark (64-bit offsets)
+    off = rng.integers((1 << 32) - 4096, size - 10000, 3000).astype(np.int64)
+    ln = rng.integers(0, 9000, 3000)
+    got = u.cksum_spans(d, dev(torch, off), dev(torch, ln.astype(np.int32)), len_hint=4000)
+    np.testing.assert_array_equal(host16(got), ora.spans(host, off, ln))
+    got = u.cksum_strided(d[(1 << 32) - 7:], 1514, 1500, 2000)
+    np.testing.assert_array_equal(
+        host16(got), ora.spans(host, (1 << 32) - 7 + 1514 * np.arange(2000), 1500))
     del d
     torch.cuda.empty_cache()
 
