@@ -123,9 +123,8 @@ int uinet_cksum_device_ok(void);
 
 /* Performance knobs (process-wide; they never change results):
  *   "blocks_per_cu"   grid-stride launch width, 0 = per-kernel default
- *   "chains_variant"  0 = pipelined chunk stream (default), 1 = serial
- *                     walk, 2 = unpipelined chunk stream
- *   "chains_pass"     passes in flight per wave in the chain kernel: 2, 4, 8
+ *   "chains_variant"  0 = pipelined chunk stream (default), 1 = serial walk
+ *   "chains_pass"     passes per batch in the chain kernel: 2, 4
  *   "chains_long"     chain segments of at least this many 16-B chunks are
  *                     streamed wave-wide; 0 = never, else >= 16 (default 128)
  *   "chains_tile"     packets per wave in the chain kernel: 0 = auto, 8, 32
@@ -137,7 +136,7 @@ int uinet_cksum_device_ok(void);
  *                     1..64 (default min(16, hardware threads))
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
- * (0|1|2, or serial|flat), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
+ * (0|1, or serial), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
  * UINET_CKSUM_CHAINS_TILE, UINET_CKSUM_XCD_REMAP, UINET_CKSUM_SPANS_LUT and
  * UINET_CKSUM_HOST_THREADS set
  * the initial values. */

@@ -65,8 +65,8 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
   };
   static const Knob knobs[] = {
       {"blocks_per_cu", &TuningLive::blocks_per_cu, [](int v) { return v >= 0 && v <= 4096; }},
-      {"chains_variant", &TuningLive::chains_variant, [](int v) { return v >= 0 && v <= 2; }},
-      {"chains_pass", &TuningLive::chains_pass, [](int v) { return v == 2 || v == 4 || v == 8; }},
+      {"chains_variant", &TuningLive::chains_variant, [](int v) { return v == 0 || v == 1; }},
+      {"chains_pass", &TuningLive::chains_pass, [](int v) { return v == 2 || v == 4; }},
       {"chains_long", &TuningLive::chains_long,
        [](int v) { return v == 0 || (v >= 16 && v <= (1 << 24)); }},
       {"chains_tile", &TuningLive::chains_tile,
@@ -95,7 +95,7 @@ static TuningLive& tuning_live() {
       const char* e = getenv(kv[0]);
       if (!e || !*e) continue;
       int v = atoi(e);
-      if (!strcmp(kv[1], "chains_variant") && (e[0] == 's' || e[0] == 'f')) v = e[0] == 's' ? 1 : 2;
+      if (!strcmp(kv[1], "chains_variant") && e[0] == 's') v = 1;  // "serial"
       if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_lut")) v = v ? 1 : 0;
       if (std::atomic<int>* f = tuning_field(*x, kv[1], v)) f->store(v, std::memory_order_relaxed);
     }

@@ -8,28 +8,28 @@
 // nothing, a short chain sums what it has), with the logical parity counted
 // from `skip`.  len == NULL means "the whole chain", skip == NULL means 0.
 //
-// k_chains_flat (UINET_CKSUM_CHAINS=flat) -- a wave owns a tile of 32 consecutive packets and
+// k_chains_pipe (default) -- a wave owns a tile of 32 consecutive packets and
 // therefore a contiguous range of segments, processed in descriptor rounds of
 // 64 segments (one per lane):
 //   * per segment: its packet slot (LDS start markers + a DPP max-scan), its
-//     chain position (a DPP segmented scan of the lengths keyed by slot,
-//     carried across rounds), the clip to [skip, len), its chunk count;
+//     chain position (a DPP add-scan of the lengths minus a max-scan of the
+//     packet-start positions, carried across rounds), the clip to
+//     [skip, len), its chunk count;
 //   * the round's segments become one concatenated list of 16-byte chunks
 //     (DPP scan of the chunk counts) that the wave sweeps 64 chunks per pass,
-//     kPass passes in flight -- every load is a dense 1 KiB whatever the
+//     kPass passes per batch -- every load is a dense 1 KiB whatever the
 //     segment lengths;
 //   * a chunk finds its segment by LDS start markers + a DPP max-scan, its
-//     bytes are masked with one ds_read_b128 from a 17x17 mask table, its
-//     fold is byte-rotated on its own (rotation is linear mod 65535);
-//   * chunk sums are binned per packet with a plain DPP prefix sum P: the
-//     last lane of each run of equal slots adds +P to its slot and -P to the
-//     next run's slot (telescoping), into the wave's u64 LDS accumulators.
+//     bytes are masked with one ds_read_b128 from a 17x17 mask table;
+//   * chunk sums are binned per (packet, parity) with a plain DPP prefix sum
+//     P: the last lane of each run of equal bins adds +P to its bin and -P to
+//     the next run's bin (telescoping), into the wave's u64 LDS accumulators;
+//     each packet's odd-parity bin is byte-rotated once at the end;
 //   * long segments (>= long_ch chunks) skip the chunk list: the whole wave
-//     streams each one like a span (no per-chunk segment lookup or binning)
-//     and adds one wave-reduced sum to its packet.
+//     streams each one like a span and adds one wave-reduced sum to its bin;
+//   * software pipelining: each batch is issued one step before it is summed.
 // Tiles of 8 packets instead of 32 when the batch is small enough that 32
 // would leave too few waves to balance 256 CUs (e.g. jumbo frames).
-// k_chains_pipe (default, below) -- k_chains_flat software-pipelined.
 // k_chains (UINET_CKSUM_CHAINS=serial, kept for A/B) -- G lanes walk one
 // packet's segments one after another.
 #include <hip/hip_runtime.h>
@@ -84,221 +84,6 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kLongU = 4;  // chunks in flight per lane on a long segment
 constexpr uint32_t kListMax = 1024;  // longest segment (chunks) the chunk list takes
 
-template <int kPass, int kTile>
-__global__ __launch_bounds__(kBlock) void k_chains_flat(const uint8_t* __restrict__ base,
-                                                       const uint64_t* __restrict__ seg_off,
-                                                       const uint32_t* __restrict__ seg_len,
-                                                       const uint32_t* __restrict__ pkt_seg,
-                                                       const uint32_t* __restrict__ plen,
-                                                       const uint32_t* __restrict__ pskip,
-                                                       const uint32_t* __restrict__ seed,
-                                                       uint16_t* __restrict__ out, uint32_t n,
-                                                       uint32_t flags, uint32_t long_ch) {
-  static_assert(kTile >= 1 && kTile <= 32,
-                "a tile's packets are one per lane, lane kTile reads the end of its segment "
-                "range, and its 2 * kTile bins are one per lane");
-  constexpr int kWin = 64 * kPass;  // chunks per batch of passes
-  __shared__ MaskLut lut;
-  // per packet two sums: bytes at even / odd logical-vs-address parity
-  // (index meta = slot * 2 + rot); the odd one is byte-rotated once at the end
-  __shared__ unsigned long long lds_acc[kWaves][2 * kTile];
-  __shared__ uint32_t lds_pkmark[kWaves][64];   // packet-start markers (slot + 1)
-  __shared__ uint8_t lds_mark[kWaves][kWin];     // segment-start markers (lane + 1)
-  lut.init();
-  for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
-  for (int i = threadIdx.x; i < kWaves * kWin; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  unsigned long long* acc = lds_acc[wid];
-  uint32_t* pkmark = lds_pkmark[wid];
-  uint8_t* mark = lds_mark[wid];
-  const uint32_t tiles = (n + kTile - 1) / kTile;
-  const uint32_t wstride = gridDim.x * kWaves;
-  // (plain block order: the XCD-banded order of the span kernels measured
-  // 1-3 % slower here, profiles/r01/ab/)
-  for (uint32_t t = blockIdx.x * kWaves + wid; t < tiles; t += wstride) {
-    const uint32_t P0 = t * kTile;
-    const int np = (int)min((uint32_t)kTile, n - P0);
-    const uint32_t ps = pkt_seg[P0 + (uint32_t)min(lane, np)];
-    const uint32_t k_skip = (lane < np && pskip) ? pskip[P0 + lane] : 0u;
-    const uint32_t k_len = (lane < np) ? (plen ? plen[P0 + lane] : 0xffffffffu) : 0u;
-    const uint32_t S0 = __builtin_amdgcn_readfirstlane(ps);
-    const uint32_t S1 = __builtin_amdgcn_readlane(ps, np);
-    if (lane < 2 * kTile) acc[lane] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    uint32_t carry_slot1 = 0;  // slot + 1 of the last segment of the previous round
-    uint32_t carry_pos = 0;    // chain offset just past that segment
-    // descriptors one round ahead: round r+1's loads fly under round r's data
-    uint64_t so_next = 0;
-    uint32_t l_next = 0;
-    auto fetch = [&](uint32_t r) {
-      const uint32_t s = r + (uint32_t)lane;
-      const uint32_t sc = s < S1 ? s : S1 - 1;
-      so_next = seg_off[sc];
-      l_next = s < S1 ? seg_len[sc] : 0u;
-    };
-    if (S0 < S1) fetch(S0);
-    for (uint32_t r0 = S0; r0 < S1; r0 += 64) {
-      // --- descriptor round: one segment per lane -------------------------
-      const uint64_t so = so_next;
-      const uint32_t l = l_next;
-      if (r0 + 64 < S1) fetch(r0 + 64);
-      // packet slot: packets starting inside this round mark their first
-      // segment; a max-scan carries the latest start to every segment
-      const bool pk_in = lane < np && ps >= r0 && ps < r0 + 64;
-      if (pk_in) atomicMax(&pkmark[ps - r0], (uint32_t)lane + 1);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      const uint32_t slot1 = max(wave_scan<1, false>(pkmark[lane], 0u), carry_slot1);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (pk_in) pkmark[ps - r0] = 0;
-      const uint32_t slot = slot1 - 1;
-      // chain position: segmented scan of the lengths, carried across rounds
-      const uint32_t pos = wave_scan<0, true>(l, slot) - l + (slot1 == carry_slot1 ? carry_pos : 0u);
-      carry_slot1 = __builtin_amdgcn_readlane(slot1, 63);
-      carry_pos = __builtin_amdgcn_readlane(pos + l, 63);
-      const uint32_t sk = __shfl(k_skip, (int)slot);
-      const uint32_t ln = __shfl(k_len, (int)slot);
-      const uint32_t lo = sk > pos ? min(sk - pos, l) : 0u;
-      const uint32_t hi = ln > pos ? min(ln - pos, l) : 0u;
-      const uint32_t eff = hi > lo ? hi - lo : 0u;
-      const uint64_t ao = so + lo;
-      const uint32_t head = eff ? (uint32_t)(reinterpret_cast<uintptr_t>(base + ao) & 15) : 0u;
-      const uint32_t nch = eff ? (head + eff + 15) >> 4 : 0u;
-      const uint64_t c0 = ao - head;  // offset of the segment's first chunk
-      const uint32_t rot = ((pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(base + ao)) & 1u;
-      const uint32_t meta = (slot << 1) | rot;
-      const uint32_t span = (eff << 4) | head;  // eff < 2^28
-      const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
-      // --- long segments: one wave-wide span each -------------------------
-      // (and any segment too long for the chunk list's 20-bit offsets)
-      const bool is_long = nch >= kListMax || (long_ch != 0 && nch >= long_ch);
-      for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
-        const int s = (int)__builtin_ctzll(lm);
-        const uint32_t sp = __builtin_amdgcn_readlane(span, s);
-        const uint32_t mts = __builtin_amdgcn_readlane(meta, s);
-        const uint8_t* cb = base + (((uint64_t)__builtin_amdgcn_readlane(c0_hi, s) << 32) |
-                                    __builtin_amdgcn_readlane(c0_lo, s));
-        const int h = (int)(sp & 15), e = h + (int)(sp >> 4);
-        const uint32_t nc = __builtin_amdgcn_readlane(nch, s);
-        uint64_t lsum = 0;
-        for (uint32_t k0 = 0; k0 < nc; k0 += 64 * kLongU) {
-          // only the passes that hold chunks are issued (wave-uniform tests)
-          u32x4 v[kLongU];
-#pragma unroll
-          for (int u = 0; u < kLongU; ++u)
-            if (u == 0 || k0 + 64u * u < nc)
-              v[u] = load_chunk(cb + 16u * min(k0 + (uint32_t)(u * 64 + lane), nc - 1));
-#pragma unroll
-          for (int u = 0; u < kLongU; ++u) {
-            if (u == 0 || k0 + 64u * u < nc) {
-              const int b = 16 * (int)(k0 + (uint32_t)(u * 64 + lane));
-              lsum += lut.sum(v[u], h - b, e - b);  // chunks past the end: [h-b, e-b) empty
-            }
-          }
-        }
-        const uint32_t x = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(lsum), 0u), 63);
-        if (lane == 0) atomicAdd(&acc[mts], (unsigned long long)x);
-      }
-      const uint32_t nch_l = is_long ? 0u : nch;  // the chunk list holds the rest
-      const uint32_t ci = wave_scan<0, false>(nch_l, 0u);
-      const uint32_t cst = ci - nch_l;  // first chunk of each segment in the round's list
-      const uint32_t C = __builtin_amdgcn_readlane(ci, 63);  // < 64 * kListMax
-      // Per list segment, what a chunk c of the list needs:
-      //   address  sbase + (dkr + 16 c) with a 32-bit offset when the round's
-      //            list segments lie within a 4 GiB window (sbase scalar), else
-      //            base + dk + 16 c in 64 bits (dk = c0 - 16 cst)
-      //   bytes    [q - 16 c, q + eff - 16 c) of the chunk   (q = head + 16 cst)
-      //   meta     slot, rotation
-      const uint32_t q0 = head + 16u * cst;  // < 2^20
-      const uint32_t recA = q0 | (meta << 20);
-      const uint32_t recB = q0 + eff;
-      const uint64_t dk = c0 - 16ull * cst;
-      const uint64_t lm_list = __ballot(nch_l != 0);
-      const int lf = lm_list ? (int)__builtin_ctzll(lm_list) : 0;
-      const uint64_t R0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(c0 >> 32), lf) << 32) |
-                          __builtin_amdgcn_readlane((uint32_t)c0, lf);
-      const uint64_t rel = c0 - R0 + (1ull << 31);  // R0 - 2 GiB .. R0 + 2 GiB
-      const bool window = __ballot(nch_l != 0 && rel >= (1ull << 32) - (1ull << 16)) == 0;
-      const uint8_t* sbase = base + (R0 - (1ull << 31));
-      const uint32_t dkr = (uint32_t)rel - 16u * cst;  // mod 2^32; + 16 c lands in range
-      // --- data: batches of kPass passes over the round's chunk list ------
-      auto sweep = [&](auto kWindow) {
-        uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the pass
-        for (uint32_t b = 0; b < C; b += kWin) {
-          const bool mk = nch_l != 0 && cst >= b && cst < b + kWin;
-          if (mk) mark[cst - b] = (uint8_t)(lane + 1);
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          u32x4 v[kPass];
-          int s_lo[kPass], s_hi[kPass];
-          uint32_t mt[kPass];
-          // segment starts of all passes at once: independent max-scans, then
-          // the carries as a scalar prefix max (seg1 never decreases)
-          uint32_t sc1[kPass];
-#pragma unroll
-          for (int q = 0; q < kPass; ++q) sc1[q] = mark[q * 64 + lane];
-#pragma unroll
-          for (int q = 0; q < kPass; ++q) sc1[q] = wave_scan<1, false>(sc1[q], 0u);
-#pragma unroll
-          for (int q = 0; q < kPass; ++q) {
-            const uint32_t last = __builtin_amdgcn_readlane(sc1[q], 63);
-            sc1[q] = max(sc1[q], carry_seg1);
-            carry_seg1 = max(carry_seg1, last);
-          }
-#pragma unroll
-          for (int q = 0; q < kPass; ++q) {
-            const uint32_t c = b + (uint32_t)(q * 64 + lane);
-            const bool in = c < C;
-            const uint32_t cc = in ? c : C - 1;  // past the end: the last chunk, masked
-            const int seg = (int)sc1[q] - 1;
-            // Cross-lane reads stay outside any condition: a ds_bpermute under
-            // a partial exec mask reads 0 from the inactive source lanes.
-            const uint32_t a = (uint32_t)__shfl(recA, seg);
-            const uint32_t bq = (uint32_t)__shfl(recB, seg);
-            mt[q] = a >> 20;
-            const int base16 = 16 * (int)c;
-            s_lo[q] = (int)(a & 0xfffffu) - base16;
-            s_hi[q] = in ? (int)bq - base16 : s_lo[q];
-            if constexpr (decltype(kWindow)::value) {
-              const uint32_t d = (uint32_t)__shfl(dkr, seg);
-              v[q] = load_chunk(sbase + (d + 16u * cc));
-            } else {
-              const uint32_t lo32 = (uint32_t)__shfl((uint32_t)dk, seg);
-              const uint32_t hi32 = (uint32_t)__shfl((uint32_t)(dk >> 32), seg);
-              v[q] = load_chunk(base + ((((uint64_t)hi32 << 32) | lo32) + 16ull * cc));
-            }
-          }
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          if (mk) mark[cst - b] = 0;
-#pragma unroll
-          for (int q = 0; q < kPass; ++q) {
-            // binned by (slot, rot): runs of equal keys, telescoping +P / -P
-            const uint32_t w = lut.sum_oc(v[q], s_lo[q], s_hi[q]);  // < 2^17
-            const uint32_t sl = mt[q];
-            const uint32_t P = wave_scan<0, false>(w, 0u);          // < 2^23
-            const uint32_t nx = wave_shl1(sl);
-            if (lane == 63 || nx != sl) {
-              atomicAdd(&acc[sl], (unsigned long long)P);
-              if (lane != 63) atomicAdd(&acc[nx], (unsigned long long)(-(long long)P));
-            }
-          }
-        }
-      };
-      if (window)
-        sweep(std::true_type());
-      else
-        sweep(std::false_type());
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (lane < np) {
-      const uint32_t p = P0 + (uint32_t)lane;
-      const uint32_t odd = fold16(acc[2 * lane + 1]);
-      out[p] = finish(acc[2 * lane] + rot8(odd) + (seed ? seed[p] : 0u), flags);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
-}
-
 // 16-B raw buffer load, non-temporal (aux bit 1), from a resource spanning
 // 4 GiB: one VGPR of offset instead of a 64-bit address per chunk.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rsrc(const uint8_t* sbase) {
@@ -309,8 +94,7 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2);
 }
 
-// k_chains_pipe (default): k_chains_flat's tile / round / chunk-list scheme,
-// software pipelined within each descriptor round.
+// k_chains_pipe: the pipelining and addressing details.
 //   * A batch is ISSUED (segment lookup, mask index and bin, loads) one step
 //     before it is CONSUMED (chunk sums, binning), so batch k+1's loads are in
 //     flight while batch k is summed.  The pipeline drains at the end of each
@@ -320,15 +104,14 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 //   * What a consumed chunk needs besides its bytes is one packed word
 //     (mask-table index | bin << 16).
 //   * Chunks within the round's 4 GiB window load through a raw buffer
-//     resource: one 32-bit VGPR offset per chunk.
-//   * Chain positions: a plain DPP add-scan of the lengths minus a max-scan
-//     of the packet-start positions (they never decrease along the round)
-//     instead of a keyed scan.
-// Measured against k_chains_flat (interleaved A/B, same process): config 3
-// +2.4-2.7 %, 3tx +1-2 %, 5tso equal.  Two things that did NOT help: an LDS
-// rank lookup of the segment records (VALU -14 %, but a second dependent LDS
-// round trip before each load: -13 %), and temporal instead of non-temporal
-// loads (HBM bytes -1.1 %, time +8 %).
+//     resource: one 32-bit VGPR offset per chunk; otherwise 64-bit addresses.
+// Against the same scheme without pipelining (k_chains_flat, removed after
+// this A/B; interleaved, same process): config 3 +2.4-2.7 %, 3tx +1-2 %, 5tso
+// equal.  Things that did NOT help: an LDS rank lookup of the segment records
+// (VALU -14 %, but a second dependent LDS round trip before each load: -13 %),
+// temporal instead of non-temporal loads (HBM bytes -1.1 %, time +8 %), an
+// XCD-banded tile order, smaller tiles at the end of the launch, a pipelined
+// long-segment stream (profiles/r01/ab/).
 template <int kPass, int kTile>
 __global__ __launch_bounds__(kBlock) void k_chains_pipe(const uint8_t* __restrict__ base,
                                                        const uint64_t* __restrict__ seg_off,
@@ -603,23 +386,18 @@ int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
 #define LF(P, T)                                                                            \
-  if (tn.chains_variant == 2)                                                                 \
-    hipLaunchKernelGGL((k_chains_flat<P, T>), dim3((int)blocks), dim3(kBlock), 0, stream, b,  \
-                       seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch);   \
-  else                                                                                        \
-    hipLaunchKernelGGL((k_chains_pipe<P, T>), dim3((int)blocks), dim3(kBlock), 0, stream, b,  \
-                       seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
+  hipLaunchKernelGGL((k_chains_pipe<P, T>), dim3((int)blocks), dim3(kBlock), 0, stream, b,    \
+                     seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
   if (tile == 8) {
-    switch (tn.chains_pass) {
-      case 4: LF(4, 8); break;
-      default: LF(2, 8); break;
-    }
+    if (tn.chains_pass == 4)
+      LF(4, 8);
+    else
+      LF(2, 8);
   } else {
-    switch (tn.chains_pass) {
-      case 8: LF(8, 32); break;
-      case 4: LF(4, 32); break;
-      default: LF(2, 32); break;
-    }
+    if (tn.chains_pass == 4)
+      LF(4, 32);
+    else
+      LF(2, 32);
   }
 #undef LF
   return check_launch();

@@ -14,8 +14,8 @@ namespace uinet {
 // a snapshot of the live values (relaxed atomics in cksum_api.hip).
 struct Tuning {
   int blocks_per_cu;   // grid-stride width
-  int chains_variant;  // 0 pipelined chunk stream, 1 serial, 2 unpipelined chunk stream
-  int chains_pass;     // 2, 4, 8
+  int chains_variant;  // 0 pipelined chunk stream, 1 serial walk
+  int chains_pass;     // 2, 4
   int host_threads;    // host-mbuf batch walk/pack threads, 1..64
   int chains_long;     // flat chains: segments of >= this many 16-B chunks stream
                        // wave-wide (0 = never)

@@ -111,10 +111,10 @@ def test_set_tuning_validation():
     """uinet_cksum_set_tuning accepts each documented knob's range and rejects
     unknown keys and out-of-range values (no device needed)."""
     L = u.lib()
-    ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_variant", 2),
+    ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_variant", 1),
           ("chains_pass", 4), ("chains_long", 0), ("chains_long", 16), ("chains_tile", 8),
           ("xcd_remap", 0), ("spans_lut", 1), ("host_threads", 64)]
-    bad = [("blocks_per_cu", -1), ("chains_variant", 3), ("chains_pass", 3), ("chains_long", 15),
+    bad = [("blocks_per_cu", -1), ("chains_variant", 2), ("chains_pass", 8), ("chains_long", 15),
            ("chains_tile", 64), ("xcd_remap", 2), ("host_threads", 0), ("no_such_knob", 1)]
     try:
         for k, v in ok:

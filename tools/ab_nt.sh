@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# Historical A/B: chains_variant 2 (k_chains_flat) and 3/4 existed only in the builds of
+# the commits that ran it; see profiles/r01/ab/*/NOTES.md for the results.
 # Chains: temporal vs non-temporal loads (variants 3 / 4), time and HBM bytes.
 set -u
 OUT=gpurun_out/${TAG:-r01i}; mkdir -p $OUT

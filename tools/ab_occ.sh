@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# Historical A/B: chains_variant 2 (k_chains_flat) and 3/4 existed only in the builds of
+# the commits that ran it; see profiles/r01/ab/*/NOTES.md for the results.
 # Chains: occupancy sensitivity (blocks per CU caps resident waves: 4 waves per
 # block, so bpc 8/6/4/2 = 8/6/4/2 waves per SIMD) for the unpipelined (2) and
 # pipelined (0) chunk-stream kernels.

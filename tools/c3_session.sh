@@ -1,4 +1,6 @@
 set -u
+# Historical A/B: chains_variant 2 (k_chains_flat) and 3/4 existed only in the builds of
+# the commits that ran it; see profiles/r01/ab/*/NOTES.md for the results.
 OUT=gpurun_out/${TAG:-r01f}; mkdir -p $OUT
 timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider -k "chains or config3 or spans or golden" > $OUT/pytest.log 2>&1; rc=$?; tail -3 $OUT/pytest.log
 case $rc in 0|1) ;; *) exit $rc;; esac
