@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -316,7 +317,8 @@ bool device_addr(const std::vector<Region>& regs, const uint8_t* p, uint32_t n,
 // pool walks in parallel, each chunk into its own piece list.  (2) A serial
 // prefix over the chunks places them.  (3) The chunks, again in parallel,
 // either write chain descriptors that point into registered memory (zero-copy:
-// the kernel folds the bytes in place over PCIe) or pack the bytes into pinned
+// the kernel folds the bytes in place over PCIe; pipelined group by group
+// with the walk) or pack the bytes into pinned
 // staging for one H2D copy and one span launch.
 
 struct Chunk {
@@ -360,9 +362,141 @@ inline bool device_addr_cached(const std::vector<Region>& regs, const uint8_t* p
   return true;
 }
 
+// zero_copy_batch's "take the staging path instead" (not a UINET_CKSUM_* code).
+constexpr int kFallback = 1;
+
+// The zero-copy batch, pipelined by groups of `threads` chunks: walk the
+// group (pool), place its chunks (serial prefix), write its chain descriptors
+// into the pinned ring (pool), launch; then the next group is walked while
+// the GPU folds this one.  Per group, in pinned memory read over PCIe:
+//   seg_off u64[np_g] | seg_len u32[np_g] | pkt_seg u32[n_g + 1] | seed u32[n_g]
+// Results land in the mapped c.h_out.  Called with g_reg_mu held and at
+// least one region registered; returns kFallback (stream drained) when a
+// group has an odd-parity start, an oversized packet or an unregistered piece.
+template <typename WalkChunk>
+int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int n,
+                    uint32_t flags, const WalkChunk& walk_chunk, bool trace) {
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = trace ? clk::now() : clk::time_point();
+  double t_walk = 0, t_desc = 0;
+  int rc = ctx_reserve(c, std::max<size_t>(c.h_cap, 1u << 20), (size_t)n);
+  if (rc) return rc;
+  uint64_t lo_addr = ~0ull;
+  for (const Region& r : g_regions) lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
+  void* dout = nullptr;
+  rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
+  if (rc) return rc;
+  void* dbuf = nullptr;
+  rc = record_hip(hipHostGetDevicePointer(&dbuf, c.h_buf, 0));
+  if (rc) return rc;
+  const std::vector<Region>& regs = g_regions;
+  const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const auto drain = [&]() { return record_hip(hipStreamSynchronize(c.stream)); };
+  const int group = std::max(1, threads);
+  size_t ring = 0;  // next free byte of the descriptor ring in c.h_buf
+  uint64_t total = 0;
+  size_t np_all = 0;
+  for (int g0 = 0; g0 < nch; g0 += group) {
+    const int g1 = std::min(nch, g0 + group);
+    clk::time_point ta = trace ? clk::now() : clk::time_point();
+    pool.run(g1 - g0, threads, [&](int jj) { walk_chunk(g0 + jj); });
+    clk::time_point tb = trace ? clk::now() : clk::time_point();
+    if (trace) t_walk += std::chrono::duration<double, std::milli>(tb - ta).count();
+
+    // place the group's chunks
+    uint64_t np64 = 0, tot_g = 0;
+    bool bad = false;
+    for (int j = g0; j < g1; j++) {
+      Chunk& C = B.chunks[(size_t)j];
+      bad |= C.odd || C.too_big;
+      C.first_piece = (uint32_t)np64;
+      np64 += C.pieces.size();
+      tot_g += C.total;
+    }
+    if (bad || np64 > 0xffffffffull) {
+      rc = drain();
+      return rc ? rc : kFallback;
+    }
+    const size_t np = (size_t)np64;
+    const int i0 = B.chunks[(size_t)g0].i0;
+    const int ng = B.chunks[(size_t)g1 - 1].i1 - i0;
+    const size_t o_len = a16(8 * np), o_ps = o_len + a16(4 * np);
+    const size_t o_sd = o_ps + a16(4 * ((size_t)ng + 1)), need = o_sd + a16(4 * (size_t)ng);
+    if (ring + need > c.h_cap) {
+      // the ring is full: wait for the launched groups, then reuse it from
+      // the start (grown to hold every remaining group at this group's size)
+      rc = drain();
+      if (rc) return rc;
+      ring = 0;
+      if (need > c.h_cap) {
+        rc = ctx_reserve(c, need * (size_t)((nch - g0 + group - 1) / group), (size_t)n);
+        if (rc) return rc;
+        rc = record_hip(hipHostGetDevicePointer(&dbuf, c.h_buf, 0));
+        if (rc) return rc;
+      }
+    }
+    uint8_t* h = c.h_buf + ring;
+    uint64_t* so = reinterpret_cast<uint64_t*>(h);
+    uint32_t* sl = reinterpret_cast<uint32_t*>(h + o_len);
+    uint32_t* ps = reinterpret_cast<uint32_t*>(h + o_ps);
+    uint32_t* sd = reinterpret_cast<uint32_t*>(h + o_sd);
+    pool.run(g1 - g0, threads, [&](int jj) {
+      Chunk& C = B.chunks[(size_t)(g0 + jj)];
+      const Region* last = nullptr;
+      const size_t k0 = C.first_piece;
+      for (size_t k = 0; k < C.pieces.size(); k++) {
+        uint64_t dev;
+        if (!device_addr_cached(regs, C.pieces[k].p, C.pieces[k].n, last, &dev)) {
+          C.unmapped = true;
+          return;
+        }
+        so[k0 + k] = dev - lo_addr;
+        sl[k0 + k] = C.pieces[k].n;
+      }
+      for (int i = C.i0; i < C.i1; i++) {
+        ps[i - i0] = C.first_piece + B.pk_first[(size_t)i];
+        sd[i - i0] = B.seed[(size_t)i];
+      }
+    });
+    ps[ng] = (uint32_t)np;
+    for (int j = g0; j < g1; j++) bad |= B.chunks[(size_t)j].unmapped;
+    if (trace) t_desc += std::chrono::duration<double, std::milli>(clk::now() - tb).count();
+    if (bad) {
+      rc = drain();
+      return rc ? rc : kFallback;
+    }
+    uint8_t* d = static_cast<uint8_t*>(dbuf) + ring;
+    rc = launch_chains(reinterpret_cast<const void*>(lo_addr),
+                       reinterpret_cast<const uint64_t*>(d),
+                       reinterpret_cast<const uint32_t*>(d + o_len),
+                       reinterpret_cast<const uint32_t*>(d + o_ps), nullptr, nullptr,
+                       reinterpret_cast<const uint32_t*>(d + o_sd),
+                       static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags,
+                       np ? (uint32_t)(tot_g / np) : 1u, c.stream);
+    if (rc) {
+      (void)drain();
+      return rc;
+    }
+    ring += need;
+    total += tot_g;
+    np_all += np;
+  }
+  const clk::time_point tw = trace ? clk::now() : clk::time_point();
+  rc = drain();
+  if (rc) return rc;
+  if (trace)
+    fprintf(stderr,
+            "uinet_cksum host batch: n=%d pieces=%zu bytes=%llu zero-copy threads=%d groups=%d "
+            "| walk %.3f descriptors %.3f (overlapped with the GPU) wait %.3f total %.3f ms\n",
+            n, np_all, (unsigned long long)total, threads, (nch + group - 1) / group, t_walk,
+            t_desc, std::chrono::duration<double, std::milli>(clk::now() - tw).count(),
+            std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+  return UINET_CKSUM_OK;
+}
+
 // Walk every packet (`walk(i, pw)` fills pw and returns the packet's seed),
-// then fold the pieces in place (all registered, even start parity) or pack
-// them into pinned staging; one launch either way.
+// then fold the pieces in place (all registered, even start parity; pipelined
+// with the walk) or pack them into pinned staging.
 template <typename WalkFn>
 int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, WalkFn walk) {
   if (n < 0) return UINET_CKSUM_EINVAL;
@@ -385,8 +519,15 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   B.par.resize((size_t)n);
   HostPool& pool = host_pool();
 
-  // (1) walk
-  pool.run(nch, threads, [&](int j) {
+  // UINET_CKSUM_TRACE_HOST=1: per-batch phase times on stderr (tools only)
+  static const bool trace = getenv("UINET_CKSUM_TRACE_HOST") != nullptr;
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t_start = trace ? clk::now() : clk::time_point();
+  clk::time_point t_walk, t_place, t_fill, t_launch;
+
+  // Walk chunk j: every packet as the reference walks it, into the chunk's
+  // piece list (pk_first chunk-local).
+  auto walk_chunk = [&](int j) {
     Chunk& C = B.chunks[(size_t)j];
     C.i0 = j * cs;
     C.i1 = std::min(n, C.i0 + cs);
@@ -405,11 +546,36 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
       C.total += nb;
       C.packed += (nb + 15) & ~uint64_t(15);
     }
-  });
+  };
 
+  // (Z) Registered memory: zero-copy, pipelined.  Groups of `threads` chunks
+  // are walked, described (12-B chain descriptors in pinned memory, packet
+  // bytes read in place over PCIe) and launched one after another, so the
+  // host walks group g+1 while the GPU folds group g.  A group whose pieces
+  // are not all registered (or that starts at an odd logical parity: the
+  // chain kernel counts parity from each packet's first byte) sends the
+  // whole batch down the staging path below.
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    if (!g_regions.empty()) {
+      rc = zero_copy_batch(c, B, pool, threads, nch, n, flags, walk_chunk, trace);
+      if (rc != kFallback) {
+        if (rc) return rc;
+        for (int i = 0; i < n; i++) {
+          if (out16) out16[i] = c.h_out[i];
+          if (out32) out32[i] = c.h_out[i];
+        }
+        return UINET_CKSUM_OK;
+      }
+    }
+  }
+
+  // (1) walk
+  pool.run(nch, threads, walk_chunk);
+
+  if (trace) t_walk = clk::now();
   // (2) place the chunks
   uint64_t total = 0, packed = 0, np64 = 0;
-  bool odd_start = false;
   for (int j = 0; j < nch; j++) {
     Chunk& C = B.chunks[(size_t)j];
     if (C.too_big) return UINET_CKSUM_EINVAL;
@@ -418,74 +584,15 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     np64 += C.pieces.size();
     total += C.total;
     packed += C.packed;
-    odd_start |= C.odd;
   }
   if (np64 > 0xffffffffull) return UINET_CKSUM_EINVAL;
   const size_t np = (size_t)np64;
   const uint32_t mean = (uint32_t)(total / (uint64_t)n);
 
-  // (3a) zero-copy when every piece is in a registered region.  (The chain
-  // kernel counts logical parity from each packet's first byte, so odd starts
-  // -- in_cksum_hdr at an odd address, out-of-contract negative pieces -- take
-  // the staging path, which carries a parity per packet.)
-  bool zero_copy = !odd_start && np > 0;
-  uint64_t lo_addr = 0;
-  if (zero_copy) {
-    std::lock_guard<std::mutex> g(g_reg_mu);
-    zero_copy = !g_regions.empty();
-    // descriptors: seg_off u64[np] | seg_len u32[np] | pkt_seg u32[n+1] | seed u32[n]
-    const size_t need = 8 * np + 4 * np + 4 * ((size_t)n + 1) + 4 * (size_t)n + 64;
-    if (zero_copy && (rc = ctx_reserve(c, need, (size_t)n)) != 0) return rc;
-    if (zero_copy) {
-      lo_addr = ~0ull;
-      for (const Region& r : g_regions)
-        lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
-      uint64_t* so = reinterpret_cast<uint64_t*>(c.h_buf);
-      uint32_t* sl = reinterpret_cast<uint32_t*>(c.h_buf + 8 * np);
-      uint32_t* ps = sl + np;
-      uint32_t* sd = ps + n + 1;
-      const std::vector<Region>& regs = g_regions;
-      pool.run(nch, threads, [&](int j) {
-        Chunk& C = B.chunks[(size_t)j];
-        const Region* last = nullptr;
-        const size_t g0 = C.first_piece;
-        for (size_t k = 0; k < C.pieces.size(); k++) {
-          uint64_t dev;
-          if (!device_addr_cached(regs, C.pieces[k].p, C.pieces[k].n, last, &dev)) {
-            C.unmapped = true;
-            return;
-          }
-          so[g0 + k] = dev - lo_addr;
-          sl[g0 + k] = C.pieces[k].n;
-        }
-        for (int i = C.i0; i < C.i1; i++) {
-          ps[i] = C.first_piece + B.pk_first[(size_t)i];
-          sd[i] = B.seed[(size_t)i];
-        }
-      });
-      ps[n] = (uint32_t)np;
-      for (int j = 0; j < nch; j++) zero_copy &= !B.chunks[(size_t)j].unmapped;
-    }
-  }
-  if (zero_copy) {
-    // Descriptors and results stay in pinned host memory too: the kernel
-    // reads/writes them over PCIe, so the batch costs one launch, no copies.
-    void* dd = nullptr;
-    void* dout = nullptr;
-    rc = record_hip(hipHostGetDevicePointer(&dd, c.h_buf, 0));
-    if (rc) return rc;
-    rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
-    if (rc) return rc;
-    uint8_t* d = static_cast<uint8_t*>(dd);
-    rc = launch_chains(reinterpret_cast<const void*>(lo_addr), reinterpret_cast<uint64_t*>(d),
-                       reinterpret_cast<uint32_t*>(d + 8 * np),
-                       reinterpret_cast<uint32_t*>(d + 12 * np), nullptr, nullptr,
-                       reinterpret_cast<uint32_t*>(d + 12 * np + 4 * ((size_t)n + 1)),
-                       static_cast<uint16_t*>(dout), (uint32_t)n, flags,
-                       (uint32_t)(total / np), c.stream);
-    if (rc) return rc;
-  } else {
-    // (3b) staging
+  if (trace) t_place = clk::now();
+  if (trace) t_fill = clk::now();
+  {
+    // (3) staging
     const Layout L = layout_for((size_t)n);
     rc = ctx_reserve(c, L.data_o + packed + 16, (size_t)n);
     if (rc) return rc;
@@ -560,8 +667,21 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
       if (rc) return rc;
     }
   }
+  if (trace) t_launch = clk::now();
   rc = record_hip(hipStreamSynchronize(c.stream));
   if (rc) return rc;
+  if (trace) {
+    const auto ms = [](clk::time_point a, clk::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const clk::time_point t_end = clk::now();
+    fprintf(stderr,
+            "uinet_cksum host batch: n=%d pieces=%zu bytes=%llu staged threads=%d | walk %.3f "
+            "place %.3f descriptors %.3f pack+launch %.3f wait %.3f ms\n",
+            n, np, (unsigned long long)total, threads,
+            ms(t_start, t_walk), ms(t_walk, t_place), ms(t_place, t_fill), ms(t_fill, t_launch),
+            ms(t_launch, t_end));
+  }
   for (int i = 0; i < n; i++) {
     if (out16) out16[i] = c.h_out[i];
     if (out32) out32[i] = c.h_out[i];

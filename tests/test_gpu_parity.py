@@ -467,6 +467,48 @@ def test_host_batch_chunked(torch_dev, ora, host_threads):
         u.set_tuning("host_threads", 16)
 
 
+@pytest.mark.parametrize("host_threads", [2, 16])
+def test_zero_copy_pipeline_ring(torch_dev, ora, host_threads):
+    """Zero-copy batches are walked and launched group by group through a
+    descriptor ring in pinned memory: on a fresh thread (1 MiB ring) 40 K
+    chains of ~8 pieces wrap the ring (2 threads: 300-KB groups) or grow it
+    (16 threads: 2-MB groups).  An odd-address header in the LAST group sends
+    a batch whose earlier groups are already launched down the staging path."""
+    rng = np.random.default_rng(300 + host_threads)
+    arena = rand_arena(1 << 22, 301)
+    seg_off, seg_len, pkt_seg = random_chain_layout(rng, 40000, arena.size, max_segs=16)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1])
+    want = ora.skip_batch(ch.heads, tot, 0)
+    hoff = rng.integers(0, arena.size - 64, 40000) & ~1
+    hoff[-1] |= 1
+    ips = arena.ctypes.data + hoff.astype(np.uint64)
+    want_hdr = ora.hdr_batch(ips)
+    got, errors = {}, []
+
+    def fresh_thread():
+        try:
+            for k in range(2):
+                got[("skip", k)] = u.in_cksum_skip_batch(ch.heads, tot, 0)
+                got[("hdr", k)] = u.in_cksum_hdr_batch(ips)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    u.set_tuning("host_threads", host_threads)
+    u.register_host(arena)
+    try:
+        t = threading.Thread(target=fresh_thread)
+        t.start()
+        t.join()
+    finally:
+        u.unregister_host(arena)
+        u.set_tuning("host_threads", 16)
+    assert not errors
+    for k in range(2):
+        np.testing.assert_array_equal(got[("skip", k)], want)
+        np.testing.assert_array_equal(got[("hdr", k)], want_hdr)
+
+
 @pytest.mark.parametrize("long_ch,tile", [(0, 32), (16, 8), (16, 32), (64, 0), (200, 8)])
 def test_chains_long_segments(torch_dev, ora, long_ch, tile):
     """Chains mixing short and long (wave-streamed) segments, with len/skip
