@@ -3,10 +3,12 @@
 //  * Device-resident descriptor API: argument checks + one launch.
 //  * Host-mbuf batch API: walks each chain exactly like the reference
 //    (/root/reference/sys/amd64/amd64/in_cksum.c:193-232 for in_cksum_skip,
-//    :241-276 for in_cksum_pseudo_header, :278-285 for in_cksum_hdr), packs
-//    the bytes each packet contributes into pinned staging (one contiguous
-//    run per packet, logical order, 16-byte aligned starts), ships staging
-//    to HBM with one copy, folds it with one launch of the span kernel and
+//    :241-276 for in_cksum_pseudo_header, :278-285 for in_cksum_hdr).  Over
+//    registered memory it writes chain descriptors and the chain kernel folds
+//    the bytes in place over PCIe, group by group while the host walks on.
+//    Otherwise it packs the bytes each packet contributes into pinned staging
+//    (one contiguous run per packet, logical order, 16-byte aligned starts),
+//    ships staging to HBM, folds it with one launch of the span kernel and
 //    copies the 16-bit results back.
 //  * Per-call drop-in ABI: a batch of one.  The reference functions have no
 //    error channel, so a HIP failure here is reported on stderr and aborts
