@@ -31,6 +31,7 @@
 #include <atomic>
 #include <chrono>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -293,7 +294,10 @@ struct Region {
   bool owned;      // registered by us (unregister on removal)
 };
 
-std::mutex g_reg_mu;
+// Batches hold it shared for as long as the GPU may read registered memory;
+// register/unregister hold it exclusive, so a region is never unmapped under
+// a running batch and concurrent batches do not serialise.
+std::shared_mutex g_reg_mu;
 std::vector<Region> g_regions;  // sorted by base, non-overlapping
 
 // Device address of [p, p + n) if it lies inside one registered region.
@@ -372,7 +376,7 @@ constexpr int kFallback = 1;
 // into the pinned ring (pool), launch; then the next group is walked while
 // the GPU folds this one.  Per group, in pinned memory read over PCIe:
 //   seg_off u64[np_g] | seg_len u32[np_g] | pkt_seg u32[n_g + 1] | seed u32[n_g]
-// Results land in the mapped c.h_out.  Called with g_reg_mu held and at
+// Results land in the mapped c.h_out.  Called with g_reg_mu held (shared) and at
 // least one region registered; returns kFallback (stream drained) when a
 // group has an odd-parity start, an oversized packet or an unregistered piece.
 template <typename WalkChunk>
@@ -558,7 +562,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   // chain kernel counts parity from each packet's first byte) sends the
   // whole batch down the staging path below.
   {
-    std::lock_guard<std::mutex> g(g_reg_mu);
+    std::shared_lock<std::shared_mutex> g(g_reg_mu);
     if (!g_regions.empty()) {
       rc = zero_copy_batch(c, B, pool, threads, nch, n, flags, walk_chunk, trace);
       if (rc != kFallback) {
@@ -755,7 +759,7 @@ int uinet_cksum_last_hip_error(void) { return t_last_hip; }
 int uinet_cksum_register_host(void* base, size_t len) {
   if (!base || len == 0) return UINET_CKSUM_EINVAL;
   const uintptr_t b = reinterpret_cast<uintptr_t>(base), e = b + len;
-  std::lock_guard<std::mutex> g(g_reg_mu);
+  std::unique_lock<std::shared_mutex> g(g_reg_mu);
   for (const Region& r : g_regions)
     if (b < r.end && r.base < e) return UINET_CKSUM_EINVAL;  // overlaps
   bool owned = true;
@@ -781,7 +785,7 @@ int uinet_cksum_register_host(void* base, size_t len) {
 
 int uinet_cksum_unregister_host(void* base) {
   const uintptr_t b = reinterpret_cast<uintptr_t>(base);
-  std::lock_guard<std::mutex> g(g_reg_mu);
+  std::unique_lock<std::shared_mutex> g(g_reg_mu);
   for (size_t i = 0; i < g_regions.size(); i++) {
     if (g_regions[i].base == b) {
       const bool owned = g_regions[i].owned;
