@@ -113,6 +113,7 @@ int grid_for(uint32_t n, int g, int bpc) {
 
 #define UINET_DISPATCH_GEOMETRY(GEO, LAUNCH)          \
   switch ((GEO).g * 16 + (GEO).u) {                   \
+    case 4 * 16 + 1: LAUNCH(4, 1); break;             \
     case 4 * 16 + 2: LAUNCH(4, 2); break;             \
     case 8 * 16 + 1: LAUNCH(8, 1); break;             \
     case 8 * 16 + 2: LAUNCH(8, 2); break;             \
@@ -158,7 +159,9 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
 int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const uint32_t* seed,
                    uint16_t* out, uint32_t n, uint32_t flags, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
-  const Geometry geo = pick_geometry(len);
+  Geometry geo = pick_geometry(len);
+  // 16-B aligned packets of at most 64 B hold at most 4 chunks: one per lane
+  if (len <= 64 && ((reinterpret_cast<uintptr_t>(base) | pkt_stride) & 15) == 0) geo = {4, 1};
   // one packet per group suits long packets; small ones want groups that
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
   const int grid = grid_for(n, geo.g, len <= 96 ? 256 : 4096);

@@ -121,7 +121,11 @@ def test_empty_batch(torch_dev):
 
 
 @pytest.mark.parametrize("stride,length,base", [(1500, 1500, 0), (1514, 1500, 14), (9000, 9000, 0),
-                                                (1501, 1500, 1), (64, 64, 0), (600, 576, 3)])
+                                                (1501, 1500, 1), (64, 64, 0), (600, 576, 3),
+                                                # 16-B aligned packets of <= 64 B (one chunk
+                                                # per lane) and their unaligned neighbours
+                                                (16, 16, 0), (48, 33, 0), (64, 1, 0), (80, 64, 16),
+                                                (64, 64, 8), (96, 63, 2)])
 def test_strided(torch_dev, ora, stride, length, base):
     torch = torch_dev
     n = 3000
