@@ -208,7 +208,9 @@ int in6_cksum_batch(struct mbuf *const *m, const uint8_t *nxt,
  * bytes all lie in registered regions is then folded in place by the GPU over
  * PCIe -- the host only walks the chains, it copies no packet bytes.  Other
  * batches are staged through pinned memory as before.  Regions must not
- * overlap; memory that is already pinned (hipHostMalloc) is accepted as is. */
+ * overlap; memory that is already pinned (hipHostMalloc) is accepted as is.
+ * Unregistering waits for the batches in flight that may read the region;
+ * batches on different threads run concurrently. */
 int uinet_cksum_register_host(void *base, size_t len);
 int uinet_cksum_unregister_host(void *base);
 

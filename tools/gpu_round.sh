@@ -11,6 +11,6 @@ step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeo
 step bench_default 600 python3 bench.py
 step trace_default 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_default" -o run --output-format csv -- python3 bench.py --cpu-baseline off
 python3 tools/pmc_summary.py "$OUT/trace_default" > "$OUT/trace_default.summary.json"
-TAG=$TAG CONFIGS="${CONFIGS:-2 2rx 2s 3 3tx 5 5tso}" bash tools/prof_all.sh || exit $?
+TAG=$TAG CONFIGS="${CONFIGS:-2 2rx 2s 3 3tx 5 5tso 2@strided 2s@strided}" bash tools/prof_all.sh || exit $?
 step hbm_read 300 tools/hbm_read
 echo "== done"

@@ -8,13 +8,16 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
   echo "   rc=$rc"; grep -v "^[EW]20" "$OUT/$name.log" | tail -n 2
   case $rc in 0) ;; *) echo FATAL; exit $rc;; esac; }
-for c in ${CONFIGS:-2 3 3tx 5 5tso}; do
-  step bench_c$c 600 python3 bench.py --config $c
-  step trace_c$c 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_c$c" -o run --output-format csv -- python3 bench.py --config $c --cpu-baseline off
-  step pmc_c$c 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_c$c" -o run --output-format csv -- python3 bench.py --config $c --steps 10 --warmup 2 --cpu-baseline off
-  read B N K <<<"$(python3 -c "import json; d=json.loads([l for l in open('$OUT/bench_c$c.log') if l.startswith('{')][-1]); print(d['config']['algorithmic_bytes_per_gpu'], d['config']['packets_per_gpu'], d['roofline']['kernel'])")"
-  python3 tools/pmc_summary.py "$OUT/pmc_c$c" --key "$K:config$c:$N" --bytes "$B" --out profiles/pmc_traffic.json > "$OUT/pmc_c$c.summary.json"
-  python3 tools/pmc_summary.py "$OUT/trace_c$c" > "$OUT/trace_c$c.summary.json"
+for spec in ${CONFIGS:-2 3 3tx 5 5tso}; do
+  # "C" (spans API) or "C@strided"
+  c=${spec%@*}; api=spans; [ "$spec" != "$c" ] && api=${spec#*@}
+  t=c$c; [ "$api" != spans ] && t=c${c}_$api
+  step bench_$t 600 python3 bench.py --config $c --api $api
+  step trace_$t 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$t" -o run --output-format csv -- python3 bench.py --config $c --api $api --cpu-baseline off
+  step pmc_$t 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$t" -o run --output-format csv -- python3 bench.py --config $c --api $api --steps 10 --warmup 2 --cpu-baseline off
+  read B N K <<<"$(python3 -c "import json; d=json.loads([l for l in open('$OUT/bench_$t.log') if l.startswith('{')][-1]); print(d['config']['algorithmic_bytes_per_gpu'], d['config']['packets_per_gpu'], d['roofline']['kernel'])")"
+  python3 tools/pmc_summary.py "$OUT/pmc_$t" --key "$K:config$c:$N" --bytes "$B" --out profiles/pmc_traffic.json > "$OUT/pmc_$t.summary.json"
+  python3 tools/pmc_summary.py "$OUT/trace_$t" > "$OUT/trace_$t.summary.json"
 done
 cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json"
 echo "== done"
