@@ -47,6 +47,9 @@ def parse():
                     "packets, a small-packet shape outside BASELINE.json)")
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU")
     ap.add_argument("--api", choices=["spans", "strided"], default="spans")
+    ap.add_argument("--desc", choices=["wide", "packed"], default="wide",
+                    help="chain configs: 12-B (uinet_cksum_chains) or packed 6-B "
+                    "(uinet_cksum_chains32) segment descriptors")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
@@ -107,11 +110,12 @@ def build_workload(cfg: str, n, rank: int):
     return w
 
 
-def make_launch(cfg: str, w, api: str, out):
+def make_launch(cfg: str, w, api: str, out, desc: str = "wide"):
     import libuinet_amd as u
 
     if cfg in CHAIN_CONFIGS:
-        return lambda s: u.cksum_chains(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"],
+        so, sl = (w["seg_off"], w["seg_len"]) if desc == "wide" else w["packed"]
+        return lambda s: u.cksum_chains(w["arena"], so, sl, w["pkt_seg"],
                                         length=w["len"], skip=w["skip"], seed=w.get("seed"),
                                         out=out, len_hint=w["hint"], stream=s)
     if api == "strided" and cfg in ("2", "2rx", "2s"):
@@ -122,9 +126,9 @@ def make_launch(cfg: str, w, api: str, out):
                                    len_hint=w["hint"], stream=s)
 
 
-def kernel_name(cfg: str, api: str) -> str:
+def kernel_name(cfg: str, api: str, desc: str = "wide") -> str:
     if cfg in CHAIN_CONFIGS:
-        return "k_chains"
+        return "k_chains32" if desc == "packed" else "k_chains"
     return "k_strided" if api == "strided" else "k_spans"
 
 
@@ -226,7 +230,9 @@ def main():
     outs = [torch.empty(n, dtype=torch.uint16, device="cuda") for _ in range(2)]
     out = outs[0]
     stream = torch.cuda.current_stream()
-    launches = [make_launch(args.config, w, args.api, o) for o in outs]
+    if args.desc == "packed" and args.config in CHAIN_CONFIGS:
+        w["packed"] = u.pack_segments(w["seg_off"], w["seg_len"])
+    launches = [make_launch(args.config, w, args.api, o, args.desc) for o in outs]
     counts = [n] * world
     rg = ResultGather(counts, "cuda") if world > 1 else None
     K, Wm = args.steps, args.warmup
@@ -287,7 +293,7 @@ def main():
         total_bytes = w["bytes"] * world * K
         value = total_bytes / elapsed / 2**30
         achieved = w["bytes"] / (kms.mean() * 1e-3) / 1e9
-        key = f"{kernel_name(args.config, args.api)}:config{args.config}:{n}"
+        key = f"{kernel_name(args.config, args.api, args.desc)}:config{args.config}:{n}"
         traffic = load_traffic(args.pmc, key)
         result = {
             "metric": metric_name(),
@@ -308,14 +314,15 @@ def main():
                 "packets_per_gpu": n,
                 "algorithmic_bytes_per_gpu": w["bytes"],
                 "api": {"spans": "uinet_cksum_spans", "strided": "uinet_cksum_strided"}[args.api]
-                if args.config not in CHAIN_CONFIGS else "uinet_cksum_chains",
+                if args.config not in CHAIN_CONFIGS else
+                {"wide": "uinet_cksum_chains", "packed": "uinet_cksum_chains32"}[args.desc],
                 "parallelism": f"dp{world} packet shards" + (
                     f" + {'RCCL' if backend == 'nccl' else backend} gather of u16 results, "
                     "overlapped with the next step's kernel" if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": kernel_name(args.config, args.api),
+                "kernel": kernel_name(args.config, args.api, args.desc),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

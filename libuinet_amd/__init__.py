@@ -29,7 +29,7 @@ __all__ = [
     "LIB_PATH", "CksumError", "lib", "in_cksum", "in_cksum_skip", "in_cksum_pseudo_header",
     "in_cksum_hdr", "in_pseudo", "in_addword", "in_cksum_skip_batch",
     "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch", "cksum_spans", "cksum_strided",
-    "cksum_chains", "F_UDP", "F_NO_COMPLEMENT", "MbufChains", "MBUF_DTYPE", "MSIZE",
+    "cksum_chains", "pack_segments", "F_UDP", "F_NO_COMPLEMENT", "MbufChains", "MBUF_DTYPE", "MSIZE",
     "SEED_BASE", "aligned_empty", "splitmix64_bytes", "EXPORTED_SYMBOLS",
 ]
 
@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "in_cksum_skip", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo", "in_addword",
     "uinet_cksum_version", "uinet_cksum_strerror", "uinet_cksum_last_hip_error",
     "uinet_cksum_device_ok", "uinet_cksum_set_tuning", "uinet_cksum_spans", "uinet_cksum_strided", "uinet_cksum_chains",
+    "uinet_cksum_chains32",
     "in_cksum_skip_batch", "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch",
     "uinet_cksum_register_host", "uinet_cksum_unregister_host",
     "uinet_cksum_rx_offload", "uinet_cksum_tx_offload",
@@ -101,6 +102,8 @@ def lib() -> ctypes.CDLL:
         "uinet_cksum_strided": (_i32, [_vp, _u64, _u32, _vp, _vp, _u32, _u32, _vp]),
         "uinet_cksum_chains": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32,
                                        _vp]),
+        "uinet_cksum_chains32": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32,
+                                         _u32, _vp]),
         "in_cksum_skip_batch": (_i32, [_vp, _vp, _vp, _vp, _i32]),
         "in_cksum_pseudo_header_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32]),
         "in_cksum_hdr_batch": (_i32, [_vp, _vp, _i32]),
@@ -322,22 +325,57 @@ def cksum_strided(base, stride: int, length: int, n: int, seed=None, out=None,
 def cksum_chains(base, seg_off, seg_len, pkt_seg, length=None, skip=None, seed=None, out=None,
                  flags: int = 0, len_hint: int = 0, stream=None):
     """``in_cksum_skip(chain_i, length[i], skip[i])`` for device-resident chains:
-    packet i = segments [pkt_seg[i], pkt_seg[i+1]) of ``base`` (int64 seg_off,
-    int32 seg_len, int32 pkt_seg of n+1 entries; optional int32 length/skip/seed)."""
+    packet i = segments [pkt_seg[i], pkt_seg[i+1]) of ``base`` (int32 pkt_seg of
+    n+1 entries; optional int32 length/skip/seed).  Wide descriptors (int64
+    seg_off, int32 seg_len) call uinet_cksum_chains; packed ones (uint32-valued
+    int32 seg_off, uint16 or uint16-valued int16 seg_len: arenas < 4 GiB,
+    mbufs <= 65535 B; see :func:`pack_segments`) call uinet_cksum_chains32."""
     import torch
 
     _dev(base, torch.uint8, "base")
-    _dev(seg_off, torch.int64, "seg_off")
-    _dev(seg_len, torch.int32, "seg_len")
+    packed = seg_off is not None and seg_off.dtype == torch.int32
+    if packed:
+        _dev(seg_off, torch.int32, "seg_off")
+        if seg_len is not None and seg_len.dtype == torch.uint16:
+            seg_len = seg_len.view(torch.int16)
+        _dev(seg_len, torch.int16, "seg_len")
+    else:
+        _dev(seg_off, torch.int64, "seg_off")
+        _dev(seg_len, torch.int32, "seg_len")
+    if seg_off.numel() != seg_len.numel():
+        raise ValueError("seg_off/seg_len size mismatch")
     _dev(pkt_seg, torch.int32, "pkt_seg")
     for t, nm in ((length, "length"), (skip, "skip"), (seed, "seed")):
         _dev(t, torch.int32, nm)
     n = pkt_seg.numel() - 1
     out = _out(n, out, base)
-    _check("uinet_cksum_chains", lib().uinet_cksum_chains(
+    fn = "uinet_cksum_chains32" if packed else "uinet_cksum_chains"
+    _check(fn, getattr(lib(), fn)(
         _dp(base), _dp(seg_off), _dp(seg_len), _dp(pkt_seg), _dp(length), _dp(skip), _dp(seed),
         _dp(out), n, flags, len_hint, _stream(stream)))
     return out
+
+
+def pack_segments(seg_off, seg_len):
+    """Wide chain descriptors (int64 offsets, int32 lengths; numpy or torch) to
+    the packed form of uinet_cksum_chains32: int32 holding the uint32 offset,
+    int16 holding the uint16 length.  Raises ValueError when an offset is not
+    below 4 GiB or a length exceeds 65535, instead of truncating."""
+    if hasattr(seg_off, "cpu"):
+        import torch
+
+        if seg_off.numel() and (int(seg_off.min()) < 0 or int(seg_off.max()) >= 1 << 32
+                                or int(seg_len.min()) < 0 or int(seg_len.max()) > 0xffff):
+            raise ValueError("segments do not fit the packed descriptor form")
+        off32 = (seg_off - ((seg_off >> 31) << 32)).to(torch.int32)
+        len16 = (seg_len - ((seg_len >> 15) << 16)).to(torch.int16)
+        return off32, len16
+    seg_off = np.asarray(seg_off, dtype=np.int64)
+    seg_len = np.asarray(seg_len, dtype=np.int64)
+    if seg_off.size and (seg_off.min() < 0 or seg_off.max() >= 1 << 32
+                         or seg_len.min() < 0 or seg_len.max() > 0xffff):
+        raise ValueError("segments do not fit the packed descriptor form")
+    return seg_off.astype(np.uint32).view(np.int32), seg_len.astype(np.uint16).view(np.int16)
 
 
 def set_tuning(key: str, value: int) -> None:

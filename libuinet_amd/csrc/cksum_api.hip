@@ -845,6 +845,17 @@ int uinet_cksum_chains(const void* base, const uint64_t* seg_off, const uint32_t
                        len_hint, static_cast<hipStream_t>(stream));
 }
 
+int uinet_cksum_chains32(const void* base, const uint32_t* seg_off, const uint16_t* seg_len,
+                         const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
+                         const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                         uint32_t len_hint, void* stream) {
+  if (n == 0) return UINET_CKSUM_OK;
+  if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
+  if (!base || !seg_off || !seg_len || !pkt_seg || !out) return UINET_CKSUM_EINVAL;
+  return launch_chains32(base, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags,
+                         len_hint, static_cast<hipStream_t>(stream));
+}
+
 // ---- host-mbuf batch API ------------------------------------------------------
 
 int in_cksum_skip_batch(struct mbuf* const* m, const int* len, const int* skip,

@@ -43,10 +43,10 @@
 namespace uinet {
 namespace {
 
-template <int G, int U>
+template <int G, int U, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) void k_chains(const uint8_t* __restrict__ base,
-                                                  const uint64_t* __restrict__ seg_off,
-                                                  const uint32_t* __restrict__ seg_len,
+                                                  const OffT* __restrict__ seg_off,
+                                                  const LenT* __restrict__ seg_len,
                                                   const uint32_t* __restrict__ pkt_seg,
                                                   const uint32_t* __restrict__ plen,
                                                   const uint32_t* __restrict__ pskip,
@@ -63,11 +63,11 @@ __global__ __launch_bounds__(kBlock) void k_chains(const uint8_t* __restrict__ b
     uint64_t tot = 0;
     uint32_t pos = 0;  // chain offset of segment s
     for (uint32_t s = s0; s < s1 && pos < hi_want; ++s) {
-      const uint32_t l = seg_len[s];
+      const uint32_t l = (uint32_t)seg_len[s];
       const uint32_t lo = lo_want > pos ? min(lo_want - pos, l) : 0u;
       const uint32_t hi = min(hi_want - pos, l);
       if (hi > lo) {
-        const uint8_t* a = base + seg_off[s] + lo;
+        const uint8_t* a = base + (uint64_t)seg_off[s] + lo;
         uint32_t x = fold16(span_lane_sum<G, U>(a, hi - lo, gl));
         const uint32_t lpar = pos + lo - lo_want;  // logical offset of a
         if ((lpar ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
@@ -112,10 +112,19 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 // temporal instead of non-temporal loads (HBM bytes -1.1 %, time +8 %), an
 // XCD-banded tile order, smaller tiles at the end of the launch, a pipelined
 // long-segment stream (profiles/r01/ab/).
-template <int kPass, int kTile>
-__global__ __launch_bounds__(kBlock) void k_chains_pipe(const uint8_t* __restrict__ base,
-                                                       const uint64_t* __restrict__ seg_off,
-                                                       const uint32_t* __restrict__ seg_len,
+// Build-time occupancy override for A/B (-DUINET_CHAINS_WAVES=7|8 forces that
+// many waves per SIMD, spilling what does not fit); unset = the compiler's 80
+// VGPRs, occupancy 6.
+#ifdef UINET_CHAINS_WAVES
+#define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(UINET_CHAINS_WAVES)))
+#else
+#define UINET_CHAINS_OCC
+#endif
+
+template <int kPass, int kTile, typename OffT, typename LenT>
+__global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const uint8_t* __restrict__ base,
+                                                       const OffT* __restrict__ seg_off,
+                                                       const LenT* __restrict__ seg_len,
                                                        const uint32_t* __restrict__ pkt_seg,
                                                        const uint32_t* __restrict__ plen,
                                                        const uint32_t* __restrict__ pskip,
@@ -178,8 +187,8 @@ __global__ __launch_bounds__(kBlock) void k_chains_pipe(const uint8_t* __restric
     auto fetch = [&](uint32_t r) {
       const uint32_t s = r + (uint32_t)lane;
       const uint32_t sc = s < S1 ? s : S1 - 1;
-      so_next = seg_off[sc];
-      l_next = s < S1 ? seg_len[sc] : 0u;
+      so_next = (uint64_t)seg_off[sc];
+      l_next = s < S1 ? (uint32_t)seg_len[sc] : 0u;
     };
     if (S0 < S1) fetch(S0);
     for (uint32_t r0 = S0; r0 < S1; r0 += 64) {
@@ -350,10 +359,13 @@ Geometry pick_serial(uint32_t mean_seg) {
 
 }  // namespace
 
-int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
-                  const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
-                  const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
-                  uint32_t len_hint, hipStream_t stream) {
+namespace {
+
+template <typename OffT, typename LenT>
+int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
+                    const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
+                    const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                    uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
   const Tuning& tn = tuning();
   const uint8_t* b = static_cast<const uint8_t*>(base);
@@ -365,7 +377,7 @@ int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg
     const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
     blocks = blocks > cap ? cap : blocks;
 #define L(G, U)                                                                              \
-  hipLaunchKernelGGL((k_chains<G, U>), dim3((int)blocks), dim3(kBlock), 0, stream, b, seg_off, \
+  hipLaunchKernelGGL((k_chains<G, U, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, b, seg_off, \
                      seg_len, pkt_seg, len, skip, seed, out, n, flags)
     switch (geo.g * 16 + geo.u) {
       case 8 * 16 + 1: L(8, 1); break;
@@ -386,7 +398,7 @@ int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
 #define LF(P, T)                                                                            \
-  hipLaunchKernelGGL((k_chains_pipe<P, T>), dim3((int)blocks), dim3(kBlock), 0, stream, b,    \
+  hipLaunchKernelGGL((k_chains_pipe<P, T, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, b,    \
                      seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
   if (tile == 8) {
     if (tn.chains_pass == 4)
@@ -401,6 +413,24 @@ int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg
   }
 #undef LF
   return check_launch();
+}
+
+}  // namespace
+
+int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
+                  const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
+                  const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                  uint32_t len_hint, hipStream_t stream) {
+  return launch_chains_t(base, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags,
+                         len_hint, stream);
+}
+
+int launch_chains32(const void* base, const uint32_t* seg_off, const uint16_t* seg_len,
+                    const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
+                    const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                    uint32_t len_hint, hipStream_t stream) {
+  return launch_chains_t(base, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags,
+                         len_hint, stream);
 }
 
 }  // namespace uinet

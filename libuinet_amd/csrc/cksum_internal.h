@@ -39,5 +39,9 @@ int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg
                   const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                   const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
                   uint32_t len_hint, hipStream_t stream);
+int launch_chains32(const void* base, const uint32_t* seg_off, const uint16_t* seg_len,
+                    const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
+                    const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                    uint32_t len_hint, hipStream_t stream);
 
 }  // namespace uinet

@@ -4,7 +4,7 @@
 set -u
 OUT=gpurun_out/${TAG:-r01ac}; mkdir -p $OUT
 cp libuinet_amd/libuinet_cksum.so $OUT/keep.so
-for rep in 1 2; do for v in A B; do
+for rep in 1 2; do for v in ${VARIANTS:-A B}; do
   cp libuinet_amd/alt/libuinet_cksum_$v.so libuinet_amd/libuinet_cksum.so
   for c in ${CONFIGS:-2 5 3 2s}; do
     timeout -k 10 300 python bench.py --config $c --api ${API:-spans} --cpu-baseline off > $OUT/b_${v}${rep}_c$c.log 2>&1 || { cp $OUT/keep.so libuinet_amd/libuinet_cksum.so; exit 1; }
