@@ -81,7 +81,10 @@ __global__ __launch_bounds__(kBlock) void k_chains(const uint8_t* __restrict__ b
 }
 
 constexpr int kWaves = kBlock / 64;
-constexpr int kLongU = 4;  // chunks in flight per lane on a long segment
+#ifndef UINET_CHAINS_LONGU  // build-time A/B knob (profiles/r01/ab/chains_occ/longu)
+#define UINET_CHAINS_LONGU 4
+#endif
+constexpr int kLongU = UINET_CHAINS_LONGU;  // chunks in flight per lane on a long segment
 constexpr uint32_t kListMax = 1024;  // longest segment (chunks) the chunk list takes
 
 // 16-B raw buffer load, non-temporal (aux bit 1), from a resource spanning
