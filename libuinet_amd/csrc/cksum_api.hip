@@ -500,11 +500,27 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   return UINET_CKSUM_OK;
 }
 
-// Walk every packet (`walk(i, pw)` fills pw and returns the packet's seed),
+// Software prefetch of the chains ahead of the walk.  The walk is bound by
+// misses on mbuf headers (m_next/m_data/m_len share the first line), each
+// dependent on the previous one, so one thread has about one miss in flight.
+// Packet i+kPfHead's head is requested; packet i+kPfNext's head (requested
+// kPfHead-kPfNext packets ago) is read to request its second mbuf, and
+// packet i+kPfNext2's second mbuf to request its third.  UINET_CKSUM_WALK_PF=0
+// turns it off (A/B only).
+constexpr int kPfHead = 16, kPfNext = 8, kPfNext2 = 4;
+
+inline void prefetch_chain(const MbufHdr* h, int depth) {
+  for (int d = 0; h && d < depth; d++) h = h->m_next;
+  if (h) __builtin_prefetch(h, 0, 3);
+}
+
+// Walk every packet (`walk(i, pw)` fills pw and returns the packet's seed;
+// `head(i)` is its first mbuf, or nullptr when there is no chain to prefetch),
 // then fold the pieces in place (all registered, even start parity; pipelined
 // with the walk) or pack them into pinned staging.
-template <typename WalkFn>
-int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, WalkFn walk) {
+template <typename WalkFn, typename HeadFn>
+int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, WalkFn walk,
+                   HeadFn head) {
   if (n < 0) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
   Ctx& c = t_ctx;
@@ -530,6 +546,10 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   using clk = std::chrono::steady_clock;
   const clk::time_point t_start = trace ? clk::now() : clk::time_point();
   clk::time_point t_walk, t_place, t_fill, t_launch;
+  static const bool prefetch = [] {
+    const char* e = getenv("UINET_CKSUM_WALK_PF");
+    return !(e && e[0] == '0');
+  }();
 
   // Walk chunk j: every packet as the reference walks it, into the chunk's
   // piece list (pk_first chunk-local).
@@ -542,6 +562,11 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     C.total = C.packed = 0;
     C.odd = C.too_big = C.unmapped = false;
     for (int i = C.i0; i < C.i1; i++) {
+      if (prefetch) {
+        if (i + kPfHead < C.i1) prefetch_chain(head(i + kPfHead), 0);
+        if (i + kPfNext < C.i1) prefetch_chain(head(i + kPfNext), 1);
+        if (i + kPfNext2 < C.i1) prefetch_chain(head(i + kPfNext2), 2);
+      }
       B.pk_first[(size_t)i] = (uint32_t)C.pieces.size();
       B.seed[(size_t)i] = walk(i, C.w);
       const uint64_t nb = C.w.bytes;
@@ -702,7 +727,7 @@ int run_jobs(const Job* jobs, int n, uint16_t* out) {
   return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
     w.walk_skip(jobs[i].m, jobs[i].len, jobs[i].skip);
     return jobs[i].seed;
-  });
+  }, [&](int i) { return jobs[i].m; });
 }
 
 namespace {
@@ -864,7 +889,7 @@ int in_cksum_skip_batch(struct mbuf* const* m, const int* len, const int* skip,
   return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
     w.walk_skip(reinterpret_cast<const MbufHdr*>(m[i]), len[i], skip[i]);
     return 0u;
-  });
+  }, [&](int i) { return reinterpret_cast<const MbufHdr*>(m[i]); });
 }
 
 int in_cksum_pseudo_header_batch(struct mbuf* const* m, const int* plen, const int* off0,
@@ -879,7 +904,7 @@ int in_cksum_pseudo_header_batch(struct mbuf* const* m, const int* plen, const i
     const uint64_t s = (uint64_t)src[i] + dst[i] + bswap16(protonum[i]) +
                        bswap16((uint16_t)plen[i]);
     return fold16_host(s);
-  });
+  }, [&](int i) { return reinterpret_cast<const MbufHdr*>(m[i]); });
 }
 
 int in6_cksum_batch(struct mbuf* const* m, const uint8_t* nxt, const uint32_t* off,
@@ -892,7 +917,7 @@ int in6_cksum_batch(struct mbuf* const* m, const uint8_t* nxt, const uint32_t* o
     const MbufHdr* mm = reinterpret_cast<const MbufHdr*>(m[i]);
     w.walk_skip(mm, (int)(off[i] + len[i]), (int)off[i]);
     return in6_pseudo_fold(mm->m_data, len[i], nxt[i]);  // "contiguous IP6 header"
-  });
+  }, [&](int i) { return reinterpret_cast<const MbufHdr*>(m[i]); });
 }
 
 int in_cksum_hdr_batch(const struct ip* const* ip, unsigned int* out, int n) {
@@ -905,7 +930,7 @@ int in_cksum_hdr_batch(const struct ip* const* ip, unsigned int* out, int n) {
     w.clen = (long)(reinterpret_cast<uintptr_t>(ip[i]) & 1);
     w.take(reinterpret_cast<const uint8_t*>(ip[i]), 20);
     return 0u;
-  });
+  }, [](int) { return static_cast<const MbufHdr*>(nullptr); });
 }
 
 // ---- drop-in per-call ABI (sys/amd64/include/in_cksum.h:76-83) --------------
