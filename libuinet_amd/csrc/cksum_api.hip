@@ -500,22 +500,59 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   return UINET_CKSUM_OK;
 }
 
-// Software prefetch of the chains ahead of the walk.  The walk is bound by
-// misses on mbuf headers (m_next/m_data/m_len share the first line), each
-// dependent on the previous one, so one thread has about one miss in flight.
-// Packet i+kPfHead's head is requested; packet i+kPfNext's head (requested
-// kPfHead-kPfNext packets ago) is read to request its second mbuf, and
-// packet i+kPfNext2's second mbuf to request its third.  UINET_CKSUM_WALK_PF=0
-// turns it off (A/B only).
-constexpr int kPfHead = 16, kPfNext = 8, kPfNext2 = 4;
+struct ChainRef {
+  const MbufHdr* m;  // first mbuf, nullptr = nothing to chase
+  long limit;        // bytes from the chain start the walk consumes
+};
 
-inline void prefetch_chain(const MbufHdr* h, int depth) {
-  for (int d = 0; h && d < depth; d++) h = h->m_next;
+// Walk prefetch.  The walk is bound by
+// misses on mbuf headers (m_next/m_data/m_len share the first line), each
+// dependent on the previous one, so walking one chain after another keeps
+// about one miss in flight per thread.  The default (prefetch_ahead) requests
+// headers a few packets ahead.  The alternative (=2, kept for A/B; equal on
+// config 3, 3-12 % slower on the offload hooks in profiles/r01/ab/walk_pf/):
+// before packets [i, i + kChase) are
+// walked, the chains of [i + kChase, i + 2 kChase) are chased side by side,
+// one mbuf of each per step: kChase independent misses in flight, and the
+// walk then finds its headers in cache.  A chase reads m_len/m_next only of
+// mbufs the walk itself reads: it stops once a chain's lengths reach the
+// bytes the packet wants from the chain start (`ChainRef::limit`).
+// UINET_CKSUM_WALK_PF=0 turns prefetching off, =2 selects the chase (A/B only).
+constexpr int kChase = 16;
+
+// Plain software prefetch ahead: packet i+16's head, i+8's second mbuf,
+// i+4's third (each read from a line an earlier step requested).
+inline void prefetch_ahead(const ChainRef& r, int depth) {
+  const MbufHdr* h = r.limit > 0 ? r.m : nullptr;
+  long rem = r.limit;
+  for (int d = 0; h && d < depth; d++) {
+    rem -= h->m_len;
+    h = rem > 0 ? h->m_next : nullptr;
+  }
   if (h) __builtin_prefetch(h, 0, 3);
 }
 
+inline void chase_chains(const ChainRef* r, int k) {
+  const MbufHdr* h[kChase];
+  long rem[kChase];
+  for (int j = 0; j < k; j++) {
+    h[j] = r[j].limit > 0 ? r[j].m : nullptr;
+    rem[j] = r[j].limit;
+  }
+  for (bool any = true; any;) {
+    any = false;
+    for (int j = 0; j < k; j++) {
+      const MbufHdr* m = h[j];
+      if (!m) continue;
+      rem[j] -= m->m_len;
+      h[j] = rem[j] > 0 ? m->m_next : nullptr;
+      any |= h[j] != nullptr;
+    }
+  }
+}
+
 // Walk every packet (`walk(i, pw)` fills pw and returns the packet's seed;
-// `head(i)` is its first mbuf, or nullptr when there is no chain to prefetch),
+// `head(i)` is the ChainRef the walk will follow, {nullptr, 0} for none),
 // then fold the pieces in place (all registered, even start parity; pipelined
 // with the walk) or pack them into pinned staging.
 template <typename WalkFn, typename HeadFn>
@@ -546,9 +583,9 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   using clk = std::chrono::steady_clock;
   const clk::time_point t_start = trace ? clk::now() : clk::time_point();
   clk::time_point t_walk, t_place, t_fill, t_launch;
-  static const bool prefetch = [] {
+  static const int prefetch = [] {  // 0 off, 1 prefetch ahead (default), 2 lockstep chase
     const char* e = getenv("UINET_CKSUM_WALK_PF");
-    return !(e && e[0] == '0');
+    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
   }();
 
   // Walk chunk j: every packet as the reference walks it, into the chunk's
@@ -561,11 +598,19 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     C.w.out = &C.pieces;
     C.total = C.packed = 0;
     C.odd = C.too_big = C.unmapped = false;
+    ChainRef refs[kChase];
+    const auto chase = [&](int a) {
+      const int k = std::min(kChase, C.i1 - a);
+      for (int j = 0; j < k; j++) refs[j] = head(a + j);
+      if (k > 0) chase_chains(refs, k);
+    };
+    if (prefetch == 2) chase(C.i0);
     for (int i = C.i0; i < C.i1; i++) {
-      if (prefetch) {
-        if (i + kPfHead < C.i1) prefetch_chain(head(i + kPfHead), 0);
-        if (i + kPfNext < C.i1) prefetch_chain(head(i + kPfNext), 1);
-        if (i + kPfNext2 < C.i1) prefetch_chain(head(i + kPfNext2), 2);
+      if (prefetch == 2 && (i - C.i0) % kChase == 0) chase(i + kChase);
+      if (prefetch == 1) {
+        if (i + 16 < C.i1) prefetch_ahead(head(i + 16), 0);
+        if (i + 8 < C.i1) prefetch_ahead(head(i + 8), 1);
+        if (i + 4 < C.i1) prefetch_ahead(head(i + 4), 2);
       }
       B.pk_first[(size_t)i] = (uint32_t)C.pieces.size();
       B.seed[(size_t)i] = walk(i, C.w);
@@ -727,7 +772,7 @@ int run_jobs(const Job* jobs, int n, uint16_t* out) {
   return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
     w.walk_skip(jobs[i].m, jobs[i].len, jobs[i].skip);
     return jobs[i].seed;
-  }, [&](int i) { return jobs[i].m; });
+  }, [&](int i) { return ChainRef{jobs[i].m, (long)jobs[i].len}; });
 }
 
 namespace {
@@ -889,7 +934,7 @@ int in_cksum_skip_batch(struct mbuf* const* m, const int* len, const int* skip,
   return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
     w.walk_skip(reinterpret_cast<const MbufHdr*>(m[i]), len[i], skip[i]);
     return 0u;
-  }, [&](int i) { return reinterpret_cast<const MbufHdr*>(m[i]); });
+  }, [&](int i) { return ChainRef{reinterpret_cast<const MbufHdr*>(m[i]), (long)len[i]}; });
 }
 
 int in_cksum_pseudo_header_batch(struct mbuf* const* m, const int* plen, const int* off0,
@@ -904,7 +949,9 @@ int in_cksum_pseudo_header_batch(struct mbuf* const* m, const int* plen, const i
     const uint64_t s = (uint64_t)src[i] + dst[i] + bswap16(protonum[i]) +
                        bswap16((uint16_t)plen[i]);
     return fold16_host(s);
-  }, [&](int i) { return reinterpret_cast<const MbufHdr*>(m[i]); });
+  }, [&](int i) {
+    return ChainRef{reinterpret_cast<const MbufHdr*>(m[i]), (long)off0[i] + plen[i]};
+  });
 }
 
 int in6_cksum_batch(struct mbuf* const* m, const uint8_t* nxt, const uint32_t* off,
@@ -917,7 +964,9 @@ int in6_cksum_batch(struct mbuf* const* m, const uint8_t* nxt, const uint32_t* o
     const MbufHdr* mm = reinterpret_cast<const MbufHdr*>(m[i]);
     w.walk_skip(mm, (int)(off[i] + len[i]), (int)off[i]);
     return in6_pseudo_fold(mm->m_data, len[i], nxt[i]);  // "contiguous IP6 header"
-  }, [&](int i) { return reinterpret_cast<const MbufHdr*>(m[i]); });
+  }, [&](int i) {
+    return ChainRef{reinterpret_cast<const MbufHdr*>(m[i]), (long)off[i] + (long)len[i]};
+  });
 }
 
 int in_cksum_hdr_batch(const struct ip* const* ip, unsigned int* out, int n) {
@@ -930,7 +979,7 @@ int in_cksum_hdr_batch(const struct ip* const* ip, unsigned int* out, int n) {
     w.clen = (long)(reinterpret_cast<uintptr_t>(ip[i]) & 1);
     w.take(reinterpret_cast<const uint8_t*>(ip[i]), 20);
     return 0u;
-  }, [](int) { return static_cast<const MbufHdr*>(nullptr); });
+  }, [](int) { return ChainRef{nullptr, 0}; });
 }
 
 // ---- drop-in per-call ABI (sys/amd64/include/in_cksum.h:76-83) --------------

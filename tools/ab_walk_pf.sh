@@ -3,7 +3,7 @@
 # the host-resident rate tools, same box, same build.
 set -u
 OUT=gpurun_out/${TAG:-abpf}; mkdir -p $OUT
-for rep in 1 2; do for v in 0 1; do
+for rep in $(seq ${REPS:-2}); do for v in ${VARIANTS:-0 1}; do
   export UINET_CKSUM_WALK_PF=$v
   timeout -k 10 300 python tests/perf/host_path.py > $OUT/host_$v$rep.log 2>&1 || exit 1
   timeout -k 10 300 python tests/perf/offload_rate.py > $OUT/offload_$v$rep.log 2>&1 || exit 1
