@@ -58,7 +58,7 @@ int check_launch() { return record_hip(hipGetLastError()); }
 // (tuning()).  The environment seeds them through the same validation.
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_variant{0}, chains_pass{2}, host_threads{8},
-      chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1};
+      chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1}, walk_prefetch{1};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -78,6 +78,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"xcd_remap", &TuningLive::xcd_remap, [](int v) { return v == 0 || v == 1; }},
       {"spans_lut", &TuningLive::spans_lut, [](int v) { return v == 0 || v == 1; }},
       {"host_threads", &TuningLive::host_threads, [](int v) { return v >= 1 && v <= 64; }},
+      {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -94,6 +95,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_CHAINS_PASS", "chains_pass"},     {"UINET_CKSUM_CHAINS_LONG", "chains_long"},
         {"UINET_CKSUM_CHAINS_TILE", "chains_tile"},     {"UINET_CKSUM_XCD_REMAP", "xcd_remap"},
         {"UINET_CKSUM_SPANS_LUT", "spans_lut"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
+        {"UINET_CKSUM_WALK_PF", "walk_prefetch"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -120,6 +122,7 @@ Tuning tuning() {
   x.chains_tile = ld(t.chains_tile);
   x.xcd_remap = ld(t.xcd_remap);
   x.spans_lut = ld(t.spans_lut);
+  x.walk_prefetch = ld(t.walk_prefetch);
   return x;
 }
 
@@ -517,7 +520,7 @@ struct ChainRef {
 // walk then finds its headers in cache.  A chase reads m_len/m_next only of
 // mbufs the walk itself reads: it stops once a chain's lengths reach the
 // bytes the packet wants from the chain start (`ChainRef::limit`).
-// UINET_CKSUM_WALK_PF=0 turns prefetching off, =2 selects the chase (A/B only).
+// Tuning knob "walk_prefetch" (env UINET_CKSUM_WALK_PF): 0 off, 1 ahead, 2 chase.
 constexpr int kChase = 16;
 
 // Plain software prefetch ahead: packet i+16's head, i+8's second mbuf,
@@ -583,10 +586,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   using clk = std::chrono::steady_clock;
   const clk::time_point t_start = trace ? clk::now() : clk::time_point();
   clk::time_point t_walk, t_place, t_fill, t_launch;
-  static const int prefetch = [] {  // 0 off, 1 prefetch ahead (default), 2 lockstep chase
-    const char* e = getenv("UINET_CKSUM_WALK_PF");
-    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
-  }();
+  const int prefetch = tuning().walk_prefetch;  // 0 off, 1 ahead (default), 2 chase
 
   // Walk chunk j: every packet as the reference walks it, into the chunk's
   // piece list (pk_first chunk-local).

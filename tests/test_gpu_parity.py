@@ -471,6 +471,42 @@ def test_host_batch_chunked(torch_dev, ora, host_threads):
         u.set_tuning("host_threads", 16)
 
 
+@pytest.mark.parametrize("walk_prefetch", [0, 1, 2])
+def test_host_walk_prefetch_variants(torch_dev, ora, walk_prefetch):
+    """Every host-walk prefetch mode gives the oracle's sums: chains longer
+    than the bytes wanted (the prefetch must stop where the walk stops), short
+    chains, len <= skip, and pseudo-header batches, staged and zero-copy."""
+    rng = np.random.default_rng(300 + walk_prefetch)
+    arena = rand_arena(1 << 22, 300)
+    seg_off, seg_len, pkt_seg = random_chain_layout(rng, 20000, arena.size, max_segs=12)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1]).astype(np.int64)
+    length = (tot * rng.uniform(0.2, 1.2, ch.n)).astype(np.int32)  # some past the chain end
+    skip = rng.integers(0, 60, ch.n).astype(np.int32)
+    want = ora.skip_batch(ch.heads, length, skip)
+    first = seg_len[pkt_seg[:-1]].astype(np.int32)
+    off0 = np.minimum(first, 20).astype(np.int32)
+    plen = np.maximum(length - off0, 0).astype(np.int32)
+    src = rng.integers(0, 2**32, ch.n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, ch.n, dtype=np.uint64).astype(np.uint32)
+    proto = np.where(rng.random(ch.n) < 0.5, 6, 17).astype(np.uint8)
+    want_ph = ora.pseudo_header_batch(ch.heads, plen, off0, src, dst, proto)
+    u.set_tuning("walk_prefetch", walk_prefetch)
+    try:
+        for registered in (False, True):
+            if registered:
+                u.register_host(arena)
+            try:
+                np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, length, skip), want)
+                np.testing.assert_array_equal(
+                    u.in_cksum_pseudo_header_batch(ch.heads, plen, off0, src, dst, proto), want_ph)
+            finally:
+                if registered:
+                    u.unregister_host(arena)
+    finally:
+        u.set_tuning("walk_prefetch", 1)
+
+
 @pytest.mark.parametrize("host_threads", [2, 16])
 def test_zero_copy_pipeline_ring(torch_dev, ora, host_threads):
     """Zero-copy batches are walked and launched group by group through a
