@@ -134,6 +134,8 @@ int uinet_cksum_device_ok(void);
  *                     sums (1, default) or register masks + 64-bit sums (0)
  *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
  *                     1..64 (default min(16, hardware threads))
+ *   "spans_contig"    span kernels: each block folds one contiguous packet
+ *                     range (1) instead of grid-wide rounds (0, default)
  *   "walk_prefetch"   host-mbuf batch walk: 0 = no prefetch, 1 = prefetch
  *                     mbuf headers a few packets ahead (default), 2 = chase
  *                     16 chains in lockstep (never changes results)
@@ -141,7 +143,7 @@ int uinet_cksum_device_ok(void);
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
  * (0|1, or serial), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
  * UINET_CKSUM_CHAINS_TILE, UINET_CKSUM_XCD_REMAP, UINET_CKSUM_SPANS_LUT,
- * UINET_CKSUM_HOST_THREADS and UINET_CKSUM_WALK_PF set
+ * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF and UINET_CKSUM_SPANS_CONTIG set
  * the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 

@@ -58,7 +58,8 @@ int check_launch() { return record_hip(hipGetLastError()); }
 // (tuning()).  The environment seeds them through the same validation.
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_variant{0}, chains_pass{2}, host_threads{8},
-      chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1}, walk_prefetch{1};
+      chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1}, walk_prefetch{1},
+      spans_contig{0};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -78,6 +79,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"xcd_remap", &TuningLive::xcd_remap, [](int v) { return v == 0 || v == 1; }},
       {"spans_lut", &TuningLive::spans_lut, [](int v) { return v == 0 || v == 1; }},
       {"host_threads", &TuningLive::host_threads, [](int v) { return v >= 1 && v <= 64; }},
+      {"spans_contig", &TuningLive::spans_contig, [](int v) { return v == 0 || v == 1; }},
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
   };
   for (const Knob& k : knobs)
@@ -95,14 +97,16 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_CHAINS_PASS", "chains_pass"},     {"UINET_CKSUM_CHAINS_LONG", "chains_long"},
         {"UINET_CKSUM_CHAINS_TILE", "chains_tile"},     {"UINET_CKSUM_XCD_REMAP", "xcd_remap"},
         {"UINET_CKSUM_SPANS_LUT", "spans_lut"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
-        {"UINET_CKSUM_WALK_PF", "walk_prefetch"},
+        {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_CONTIG", "spans_contig"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
       if (!e || !*e) continue;
       int v = atoi(e);
       if (!strcmp(kv[1], "chains_variant") && e[0] == 's') v = 1;  // "serial"
-      if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_lut")) v = v ? 1 : 0;
+      if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_lut") ||
+          !strcmp(kv[1], "spans_contig"))
+        v = v ? 1 : 0;
       if (std::atomic<int>* f = tuning_field(*x, kv[1], v)) f->store(v, std::memory_order_relaxed);
     }
     return x;
@@ -123,6 +127,7 @@ Tuning tuning() {
   x.xcd_remap = ld(t.xcd_remap);
   x.spans_lut = ld(t.spans_lut);
   x.walk_prefetch = ld(t.walk_prefetch);
+  x.spans_contig = ld(t.spans_contig);
   return x;
 }
 

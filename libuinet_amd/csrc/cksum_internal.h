@@ -22,6 +22,7 @@ struct Tuning {
   int chains_tile;     // flat chains: packets per wave tile, 0 = auto, 8, 32
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
   int spans_lut;       // span kernels: LDS mask table + one's-complement sums (0/1)
+  int spans_contig;    // span kernels: block-contiguous packet ranges (0/1)
   int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead, 2 lockstep chase
 };
 Tuning tuning();

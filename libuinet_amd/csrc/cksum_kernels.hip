@@ -36,13 +36,27 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
                                                  const uint8_t* __restrict__ parity,
                                                  uint64_t pkt_stride, uint32_t fixed_len,
                                                  uint16_t* __restrict__ out, uint32_t n,
-                                                 uint32_t flags, uint32_t remap) {
+                                                 uint32_t flags, uint32_t remap,
+                                                 uint32_t contig) {
   constexpr uint32_t kGroups = kBlock / G;
   __shared__ MaskLut lut;
   const int gl = threadIdx.x & (G - 1);
-  const uint32_t stride = gridDim.x * kGroups;
-  uint32_t p = logical_block(remap) * kGroups + threadIdx.x / G;
-  const bool live = p < n;
+  // contig = 0: round r of the grid covers packets [r S, (r + 1) S), S = the
+  // grid's group count (a group's packets lie S apart).  contig = 1: block b
+  // owns the contiguous range [b C, (b + 1) C), C = kGroups * ceil(n / S),
+  // and its groups step through it kGroups apart.  Interleaved A/B on one box
+  // (profiles/r01/ab/contig/): config 2 -1.1 %, 2rx -1.0 %, 5 equal, 64-B
+  // packets +1.1 %; the default stays 0.
+  const uint32_t S = gridDim.x * kGroups;
+  const uint32_t lb = logical_block(remap);
+  uint32_t stride = S, p = lb * kGroups + threadIdx.x / G, pend = n;
+  if (contig) {
+    const uint32_t chunk = ((n + S - 1) / S) * kGroups;
+    stride = kGroups;
+    p = lb * chunk + threadIdx.x / G;
+    pend = min(n, lb * chunk + chunk);
+  }
+  const bool live = p < pend;
   uint64_t o = 0;
   uint32_t l = 0;
   if (live) {
@@ -75,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
     if ((lp ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
     x = group_sum<G>(x);
     if (gl == 0) out[p] = finish((uint64_t)x + (seed ? seed[p] : 0u), flags);
-    if (pn >= n) break;
+    if (pn >= pend) break;
     p = pn;
     o = on;
     l = ln;
@@ -146,11 +160,13 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   if (tuning().spans_lut)                                                                \
     hipLaunchKernelGGL((k_spans<G, U, false, true>), dim3(grid), dim3(kBlock), 0, stream, \
                        static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
-                       out, n, flags, (uint32_t)tuning().xcd_remap);                     \
+                       out, n, flags, (uint32_t)tuning().xcd_remap,                      \
+                       (uint32_t)tuning().spans_contig);                                 \
   else                                                                                   \
     hipLaunchKernelGGL((k_spans<G, U, false, false>), dim3(grid), dim3(kBlock), 0, stream, \
                        static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
-                       out, n, flags, (uint32_t)tuning().xcd_remap)
+                       out, n, flags, (uint32_t)tuning().xcd_remap,                      \
+                       (uint32_t)tuning().spans_contig)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
@@ -169,11 +185,13 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   if (tuning().spans_lut)                                                               \
     hipLaunchKernelGGL((k_spans<G, U, true, true>), dim3(grid), dim3(kBlock), 0, stream, \
                        static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
-                       pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap);    \
+                       pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap,     \
+                       (uint32_t)tuning().spans_contig);                                 \
   else                                                                                  \
     hipLaunchKernelGGL((k_spans<G, U, true, false>), dim3(grid), dim3(kBlock), 0, stream, \
                        static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
-                       pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap)
+                       pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap,     \
+                       (uint32_t)tuning().spans_contig)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();

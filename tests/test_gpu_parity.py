@@ -84,6 +84,30 @@ def test_spans_no_seed_no_parity(torch_dev, ora, hint):
     np.testing.assert_array_equal(host16(got), want)
 
 
+@pytest.mark.parametrize("n", [1, 7, 6000, 70001])
+def test_spans_contig_order(torch_dev, ora, n):
+    """Block-contiguous packet order (spans_contig=1) at every geometry and
+    for the strided kernel: every packet folded exactly once, ragged tails."""
+    torch = torch_dev
+    rng = np.random.default_rng(500 + n)
+    arena = rand_arena(1 << 21, 31)
+    off, ln = rand_spans(rng, n, arena.size, 1600)
+    want = ora.spans(arena, off, ln)
+    d_arena = dev(torch, arena)
+    u.set_tuning("spans_contig", 1)
+    try:
+        for hint in HINTS:
+            got = u.cksum_spans(d_arena, dev(torch, off), dev(torch, ln.astype(np.int32)),
+                                len_hint=hint)
+            np.testing.assert_array_equal(host16(got), want)
+        m = min(n, (arena.size - 64) // 64)
+        got = u.cksum_strided(d_arena, 64, 60, m)
+        want_s = ora.spans(arena, 64 * np.arange(m, dtype=np.int64), np.full(m, 60, np.int64))
+        np.testing.assert_array_equal(host16(got), want_s)
+    finally:
+        u.set_tuning("spans_contig", 0)
+
+
 def test_spans_long(torch_dev, ora):
     """Spans far longer than one unrolled round of any geometry."""
     torch = torch_dev
