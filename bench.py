@@ -6,8 +6,14 @@ HBM: a single launch of the engine's span kernel (``uinet_cksum_spans``, the
 C ABI the libuinet shim calls) over the rank's packets, plus -- for N > 1 --
 the one RCCL gather of the 16-bit results to rank 0.  Workload at N = 1 is
 BASELINE.json configs[1] (config 2): 1,048,576 x 1500-B contiguous packets,
-in_cksum_skip(m, 1500, 0).  For N > 1 every rank folds its own 1,048,576
-packets (weak scaling; config 4's 2,097,152 per GPU is ``--packets 2097152``).
+in_cksum_skip(m, 1500, 0).  For N > 1 the default is config 4 (configs[3]):
+every rank folds its own 2,097,152 x 1500-B packets (16 M over 8 GPUs, weak
+scaling) and the u16 results meet on rank 0 in one gather per step.
+
+Launch: ``python bench.py --gpus N``.  Without a launcher (no WORLD_SIZE in
+the environment) and N > 1, this process starts N ranks itself with
+``torch.distributed.run`` as a child process -- before anything touches the
+GPU -- and exits with its status; under torchrun WORLD_SIZE must equal N.
 
 Rank 0 prints ONE JSON line.  ``roofline`` prices the span kernel: algorithmic
 bytes per launch (sum of packet lengths) / its mean HIP-event duration on the
@@ -42,9 +48,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=200,
                     help="untimed steps first: the first ~30-100 back-to-back launches run "
                     "up to 25 %% slower while clocks settle (tools/drift.py)")
-    ap.add_argument("--config", choices=["2", "2rx", "2s", "3", "3tx", "5", "5tso"], default="2",
-                    help="BASELINE.json config shape (2 = the headline; 2s = 16 M x 64 B "
-                    "packets, a small-packet shape outside BASELINE.json)")
+    ap.add_argument("--config", choices=["2", "2rx", "2s", "3", "3tx", "4", "5", "5tso"],
+                    default=None,
+                    help="BASELINE.json config shape (default: 2 = the headline at N = 1, 4 = "
+                    "2,097,152 packets per GPU when distributed; 2s = 16 M x 64 B packets, a "
+                    "small-packet shape outside BASELINE.json)")
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU")
     ap.add_argument("--api", choices=["spans", "strided"], default="spans")
     ap.add_argument("--desc", choices=["wide", "packed"], default="wide",
@@ -56,7 +64,35 @@ def parse():
                     help="per-launch HBM traffic measured by rocprofv3 --pmc")
     ap.add_argument("--host-path", action="store_true",
                     help="also time H2D + kernel + D2H (host-resident rate)")
+    ap.add_argument("--save-results", default=None, metavar="NPY",
+                    help="rank 0 saves the last timed step's u16 results (every rank's, "
+                    "gathered, in rank order) to this .npy file")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch (and rendezvous, over gloo) as usual, print each rank's plan "
+                    "as JSON and exit before touching the GPU")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start ``n`` ranks of this script under torch.distributed.run as a
+    child process (never an exec: nothing here has touched the GPU, and the
+    box forbids replacing a process) and return its exit status."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+    return subprocess.run(cmd, env=env).returncode
 
 
 def metric_name() -> str:
@@ -67,10 +103,17 @@ def metric_name() -> str:
         return "device-resident checksum GiB/s"
 
 
-def build_workload(cfg: str, n, rank: int):
+def build_workload(cfg: str, n, rank: int, world: int = 1):
     import libuinet_amd.workloads as W
 
-    if cfg in ("2", "2rx"):
+    if cfg == "4":
+        n = n or (1 << 21)
+        w = W.config2_device(n, rank=rank)
+        w["desc"] = (f"config4: {n * world:,} x 1500 B packets sharded {n:,} per GPU over "
+                     f"{world} GPU{'s' if world > 1 else ''} (stride 1500, device-resident), "
+                     f"in_cksum_skip(m,1500,0); u16 results gathered to rank 0")
+        w["hint"] = 1500
+    elif cfg in ("2", "2rx"):
         n = n or (1 << 20)
         w = W.config2_device(n, stride=1514 if cfg == "2rx" else 1500,
                              base=14 if cfg == "2rx" else 0, rank=rank)
@@ -142,6 +185,19 @@ def load_traffic(path: str, key: str):
         return None
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:  # pragma: no cover
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(cfg: str, w, gpu_out, threads: int):
     """The reference's scalar in_cksum_skip / in_cksum_pseudo_header over the same
     bytes as host mbufs; returns the cpu_baseline object (and checks parity)."""
@@ -191,6 +247,7 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
     parity = bool(np.array_equal(outn, gpu_out) and np.array_equal(out1, gpu_out))
     return {
         "value": round(gib / tn, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "cpu_model": cpu_model(),
         "sample": (f"{w['n']:,} packets ({gib:.3f} GiB algorithmic) of the benchmarked batch, "
                    f"host copy as {'chained ' if cfg in CHAIN_CONFIGS else ''}struct mbuf; best of 5 on "
                    f"{threads} pinned threads; 1 thread: {gib / t1:.3f} GiB/s best of 3; "
@@ -202,29 +259,54 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # the ranks print the JSON line
+    distributed = env_world is not None
+    if distributed and int(env_world) != args.gpus:
+        sys.exit(f"bench: --gpus {args.gpus} but WORLD_SIZE={env_world}; launch with "
+                 f"torchrun --nproc-per-node {args.gpus} (or drop the launcher)")
+    if args.config is None:
+        args.config = "4" if distributed else "2"
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if distributed:
+            dist.init_process_group("gloo")
+        plan = {"rank": rank, "local_rank": local,
+                "world": dist.get_world_size() if distributed else 1, "config": args.config,
+                "packets_per_gpu": args.packets or {"4": 1 << 21, "2s": 1 << 24,
+                                                    "5": 131072}.get(args.config, 1 << 20),
+                "backend": os.environ.get("UINET_BENCH_BACKEND", "nccl") if distributed else None}
+        print(json.dumps(plan), flush=True)
+        if distributed:
+            dist.destroy_process_group()
+        return
     # UINET_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
     # one GPU (CI / 1-GPU boxes); the real runs use RCCL, one rank per GPU.
     backend = os.environ.get("UINET_BENCH_BACKEND", "nccl")
-    dev = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and local >= ndev:
+        sys.exit(f"bench: rank {rank} has LOCAL_RANK {local} but {ndev} GPU(s) are visible "
+                 "(RCCL needs one GPU per rank; UINET_BENCH_BACKEND=gloo shares one)")
+    dev = local % max(1, ndev)
     torch.cuda.set_device(dev)
-    if world > 1:
+    if distributed:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
+    world = dist.get_world_size() if distributed else 1
 
     import libuinet_amd as u
     from libuinet_amd.dist import ResultGather
 
     if not u.device_ok():
         raise SystemExit("bench: no gfx950 device visible")
-    w = build_workload(args.config, args.packets, rank)
+    w = build_workload(args.config, args.packets, rank, world)
     n = w["n"]
     # two result buffers: step k's gather overlaps step k+1's kernel (N > 1)
     outs = [torch.empty(n, dtype=torch.uint16, device="cuda") for _ in range(2)]
@@ -234,13 +316,13 @@ def main():
         w["packed"] = u.pack_segments(w["seg_off"], w["seg_len"])
     launches = [make_launch(args.config, w, args.api, o, args.desc) for o in outs]
     counts = [n] * world
-    rg = ResultGather(counts, "cuda") if world > 1 else None
+    rg = ResultGather(counts, "cuda") if distributed else None
     K, Wm = args.steps, args.warmup
     # Kernel time from HIP events on the launch stream.  At N = 1 a step IS
     # one launch, so one event pair brackets the K back-to-back launches (no
     # per-launch event overhead; inter-launch gaps count against us).  At
     # N > 1 each launch is bracketed so the gather stays out of it.
-    per_launch = world > 1
+    per_launch = distributed
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(K if per_launch else 1)]
 
@@ -261,7 +343,7 @@ def main():
     if rg is not None:
         rg.wait_all()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -274,11 +356,11 @@ def main():
     if rg is not None:
         rg.wait_all()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -318,7 +400,8 @@ def main():
                 {"wide": "uinet_cksum_chains", "packed": "uinet_cksum_chains32"}[args.desc],
                 "parallelism": f"dp{world} packet shards" + (
                     f" + {'RCCL' if backend == 'nccl' else backend} gather of u16 results, "
-                    "overlapped with the next step's kernel" if world > 1 else ""),
+                    "overlapped with the next step's kernel" if distributed else ""),
+                "launcher": "torch.distributed.run" if distributed else "none",
             },
             "roofline": {
                 "bound": "hbm",
@@ -339,9 +422,13 @@ def main():
         torch.cuda.synchronize()
         gpu_out = outs[(K - 1) & 1].cpu().view(torch.int16).numpy().view(np.uint16)
         result["cpu_baseline"] = cpu_baseline(args.config, w, gpu_out, args.cpu_threads)
+    if args.save_results and rank == 0:
+        last = (K - 1) & 1
+        res = rg.result(last) if rg is not None else outs[last].view(torch.int16)
+        np.save(args.save_results, res.cpu().numpy().view(np.uint16))
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 

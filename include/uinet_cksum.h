@@ -7,18 +7,20 @@
  *     signatures of /root/reference/sys/amd64/include/in_cksum.h:44,76-83 (the
  *     object the amd64 build compiles, sys/amd64/amd64/in_cksum.c).  Linking
  *     libuinet_cksum in place of that object keeps lib/libuinet and
- *     bin/multitool unchanged.  The data-touching entry points
- *     run on the GPU (a batch of one, synchronous).
+ *     bin/multitool unchanged.  One call folds one chain on
+ *     the calling CPU thread: a synchronous GPU round trip per packet would be
+ *     ~30x slower than the fold, and these functions, like the reference,
+ *     have no error path -- they never touch the device and never fail.
  *
  *  2. Batch entry points for callers that hold many packets at once
  *     (the RX/TX driver batches of SURVEY.md section 8f), and the
  *     device-resident descriptor API that is the hot path proper: one HIP
  *     launch folds a whole batch of packets that already sit in HBM.
  *
- * Results are bit-identical to the reference on the same inputs.  Nothing
- * here silently falls back to a CPU computation: the batch and device entry
- * points return a negative UINET_CKSUM_E* code, the per-call ABI (which has no
- * error channel, like the reference) prints the HIP error and aborts.
+ * Results are bit-identical to the reference on the same inputs.  The batch,
+ * device and offload entry points (section 2) are the GPU engine and never
+ * fall back to a CPU computation: without a usable gfx950 device they return
+ * a negative UINET_CKSUM_E* code.
  */
 #ifndef UINET_CKSUM_H
 #define UINET_CKSUM_H
@@ -87,6 +89,18 @@ uinet_in_cksum_update(void *ip_hdr)
 	p[0] = (unsigned char)(s >> 8);
 	p[1] = (unsigned char)s;
 }
+
+/* The reference's own name and type (in_cksum.h:46-61: defined when
+ * <netinet/ip.h> has set IPVERSION 4), for code that includes this header
+ * instead of <machine/in_cksum.h>; a translation unit that includes the
+ * reference header keeps the reference's definition. */
+#if defined(IPVERSION) && (IPVERSION == 4) && !defined(_MACHINE_IN_CKSUM_H_)
+static inline void
+in_cksum_update(struct ip *ip)
+{
+	uinet_in_cksum_update(ip);
+}
+#endif
 
 /* IPv6 (sys/netinet6/in6.h:637-638, compiled
  * by the reference only with INET6).  in6_cksum.c:150-357: the transport
@@ -160,6 +174,11 @@ int uinet_cksum_set_tuning(const char *key, int value);
 /* ------------------------------------------------------------------------ */
 
 #define UINET_CKSUM_MAX_PACKETS 0x80000000u
+/* Longest span the span/strided kernels fold (their in-span byte positions
+ * are 32-bit signed, like the reference's `int len`): len[i] must be below
+ * this; uinet_cksum_strided returns UINET_CKSUM_EINVAL for a longer len.
+ * Chain segments (uinet_cksum_chains) may hold up to 2^32 - 1 bytes. */
+#define UINET_CKSUM_MAX_SPAN 0x7ffff000u
 
 /* One contiguous span per packet:
  *   out[i] = checksum of bytes [base + off[i], base + off[i] + len[i])
@@ -272,6 +291,44 @@ int uinet_cksum_rx_offload(struct mbuf *const *m, int n, int l2len,
  * ip_sum store (:665-667) do, then clears those csum_flags bits. */
 int uinet_cksum_tx_offload(struct mbuf *const *m, int n, int l2len,
     uint8_t *status);
+
+/* ------------------------------------------------------------------------ */
+/* 2e. Multi-device batches                           */
+/*                                                                          */
+/* Packets are independent, so a batch shards across GPUs with no exchange  */
+/* but the results.  Each shard runs on its own host thread with its own    */
+/* stream on its device; shards may share a device.  Both calls are         */
+/* synchronous and thread-safe.                                             */
+/* ------------------------------------------------------------------------ */
+
+/* One device-resident shard: the span batch of uinet_cksum_spans, its
+ * pointers on `device`. */
+struct uinet_cksum_shard {
+	int device;
+	uint32_t n;
+	const void *base;
+	const uint64_t *off;
+	const uint32_t *len;
+	const uint32_t *seed;    /* may be NULL */
+	const uint8_t *parity;   /* may be NULL */
+};
+
+/* Folds every shard on its own device (the span kernel, as
+ * uinet_cksum_spans) and gathers the 16-bit results into root_out, a device
+ * pointer on root_device: shard k's results start at the sum of the n of
+ * shards 0..k-1.  The gather is a peer copy over xGMI (on-device when a
+ * shard lives on root_device).  Returns when every result is in root_out. */
+int uinet_cksum_spans_multi(const struct uinet_cksum_shard *shards, int nshards,
+    uint32_t flags, uint32_t len_hint, int root_device, uint16_t *root_out);
+
+/* A host-mbuf batch (in_cksum_skip_batch semantics) over ndev devices: the
+ * packets are cut into ndev contiguous ranges of about equal summed bytes
+ * (len[i] - skip[i]); range j is walked, staged (or read in place from
+ * registered memory) and folded on devices[j], and its results land in out[]
+ * at their own indices.  For libuinet's per-interface RX/TX threads
+ * (uinet_if_netmap.c:1652-1665) on a multi-GPU host. */
+int in_cksum_skip_batch_multi(const int *devices, int ndev, struct mbuf *const *m,
+    const int *len, const int *skip, unsigned short *out, int n);
 
 #if defined(__GNUC__)
 #pragma GCC visibility pop

@@ -30,7 +30,8 @@ __all__ = [
     "in_cksum_hdr", "in_pseudo", "in_addword", "in_cksum_skip_batch",
     "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch", "cksum_spans", "cksum_strided",
     "cksum_chains", "pack_segments", "F_UDP", "F_NO_COMPLEMENT", "MbufChains", "MBUF_DTYPE", "MSIZE",
-    "SEED_BASE", "aligned_empty", "splitmix64_bytes", "EXPORTED_SYMBOLS",
+    "SEED_BASE", "aligned_empty", "splitmix64_bytes", "EXPORTED_SYMBOLS", "cksum_spans_multi",
+    "in_cksum_skip_batch_multi",
 ]
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libuinet_cksum.so")
@@ -51,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "uinet_cksum_register_host", "uinet_cksum_unregister_host",
     "uinet_cksum_rx_offload", "uinet_cksum_tx_offload",
     "in6_cksum", "in6_cksum_pseudo", "in6_cksum_batch",
+    "uinet_cksum_spans_multi", "in_cksum_skip_batch_multi",
 )
 
 # Driver offload status bits (include/uinet_cksum.h section 2d).
@@ -114,6 +116,8 @@ def lib() -> ctypes.CDLL:
         "in6_cksum": (_i32, [_vp, _u8, _u32, _u32]),
         "in6_cksum_pseudo": (_i32, [_vp, _u32, _u8, _u16]),
         "in6_cksum_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32]),
+        "uinet_cksum_spans_multi": (_i32, [_vp, _i32, _u32, _u32, _i32, _vp]),
+        "in_cksum_skip_batch_multi": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -376,6 +380,60 @@ def pack_segments(seg_off, seg_len):
                          or seg_len.min() < 0 or seg_len.max() > 0xffff):
         raise ValueError("segments do not fit the packed descriptor form")
     return seg_off.astype(np.uint32).view(np.int32), seg_len.astype(np.uint16).view(np.int16)
+
+
+class Shard(ctypes.Structure):
+    """struct uinet_cksum_shard (include/uinet_cksum.h section 2e)."""
+
+    _fields_ = [("device", ctypes.c_int), ("n", ctypes.c_uint32), ("base", _vp), ("off", _vp),
+                ("len", _vp), ("seed", _vp), ("parity", _vp)]
+
+
+def cksum_spans_multi(shards, root_device: int = 0, out=None, flags: int = 0,
+                      len_hint: int = 0):
+    """uinet_cksum_spans_multi: ``shards`` is a list of dicts with device tensors
+    ``base`` (uint8), ``off`` (int64), ``length`` (int32) and optional ``seed``
+    (int32) / ``parity`` (uint8), each on its own device; returns the gathered
+    uint16 results on ``root_device`` (shard order)."""
+    import torch
+
+    arr = (Shard * len(shards))()
+    total = 0
+    for k, sh in enumerate(shards):
+        base, off, ln = sh["base"], sh["off"], sh["length"]
+        _dev(base, torch.uint8, "base")
+        _dev(off, torch.int64, "off")
+        _dev(ln, torch.int32, "length")
+        _dev(sh.get("seed"), torch.int32, "seed")
+        _dev(sh.get("parity"), torch.uint8, "parity")
+        if off.numel() != ln.numel():
+            raise ValueError("off/length size mismatch")
+        arr[k] = Shard(base.device.index, off.numel(), _dp(base), _dp(off), _dp(ln),
+                       _dp(sh.get("seed")), _dp(sh.get("parity")))
+        total += off.numel()
+    if out is None:
+        out = torch.empty(total, dtype=torch.uint16, device=f"cuda:{root_device}")
+    _dev(out, torch.uint16, "out")
+    if out.numel() < total or out.device.index != root_device:
+        raise ValueError("out must hold every result on root_device")
+    for sh in shards:  # the shards' inputs were written on the callers' streams
+        torch.cuda.synchronize(sh["base"].device)
+    _check("uinet_cksum_spans_multi", lib().uinet_cksum_spans_multi(
+        ctypes.addressof(arr), len(shards), flags, len_hint, root_device, _dp(out)))
+    return out
+
+
+def in_cksum_skip_batch_multi(devices, heads, length, skip) -> np.ndarray:
+    """in_cksum_skip_batch spread over ``devices`` (byte-balanced contiguous ranges)."""
+    devs = np.ascontiguousarray(devices, dtype=np.int32)
+    heads = np.ascontiguousarray(heads, dtype=np.uint64)
+    n = heads.size
+    length = np.ascontiguousarray(np.broadcast_to(length, (n,)), dtype=np.int32)
+    skip = np.ascontiguousarray(np.broadcast_to(skip, (n,)), dtype=np.int32)
+    out = np.zeros(n, dtype=np.uint16)
+    _check("in_cksum_skip_batch_multi", lib().in_cksum_skip_batch_multi(
+        _ptr(devs), devs.size, _ptr(heads), _ptr(length), _ptr(skip), _ptr(out), n))
+    return out
 
 
 def set_tuning(key: str, value: int) -> None:

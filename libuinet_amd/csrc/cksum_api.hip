@@ -10,9 +10,8 @@
 //    (one contiguous run per packet, logical order, 16-byte aligned starts),
 //    ships staging to HBM, folds it with one launch of the span kernel and
 //    copies the 16-bit results back.
-//  * Per-call drop-in ABI: a batch of one.  The reference functions have no
-//    error channel, so a HIP failure here is reported on stderr and aborts
-//    rather than returning a made-up checksum.
+//  * Per-call drop-in ABI: one chain folded on the calling thread
+//    (cksum_percall.cpp); no device, no error path, like the reference.
 //
 // Threading: the reference checksum is fully reentrant; here
 // every calling thread gets its own stream and staging buffers (thread_local),
@@ -154,38 +153,57 @@ struct Ctx {
   size_t out_cap = 0;
 };
 
-// Staging is intentionally not released at thread exit: HIP may already be
-// torn down when the main thread's thread_local destructors run.
-thread_local Ctx t_ctx;
+// One context per (thread, device): a thread that serves several devices --
+// the multi-device batch workers (cksum_multi.hip), or a caller that switches
+// with hipSetDevice -- keeps every device's stream and staging instead of
+// dropping and rebuilding them.  Staging is intentionally not released at
+// thread exit: HIP may already be torn down when the main thread's
+// thread_local destructors run.
+constexpr int kMaxDevices = 64;
+thread_local Ctx t_ctx[kMaxDevices];
 
-int ctx_ready(Ctx& c) {
+// The calling thread's context for its current device, stream created.
+int ctx_current(Ctx** out) {
   int dev = 0;
   int rc = record_hip(hipGetDevice(&dev));
   if (rc) return rc;
-  if (c.device == dev && c.stream) return UINET_CKSUM_OK;
-  if (c.device != dev && c.stream) {  // thread switched devices: start over
-    c = Ctx();
+  if (dev < 0 || dev >= kMaxDevices) return UINET_CKSUM_ENODEV;
+  Ctx& c = t_ctx[dev];
+  if (!c.stream) {
+    rc = record_hip(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    if (rc) return rc;
+    c.device = dev;
   }
-  rc = record_hip(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-  if (rc) return rc;
-  c.device = dev;
+  *out = &c;
   return UINET_CKSUM_OK;
 }
 
-int ctx_reserve(Ctx& c, size_t bytes, size_t nout) {
+// Grows the pinned staging to `bytes` (and its HBM mirror when `device`: the
+// zero-copy path reads pinned memory in place and needs none) and the result
+// buffers to `nout` entries.
+int ctx_reserve(Ctx& c, size_t bytes, size_t nout, bool device = true) {
+  const auto grow = [](size_t cap, size_t want) {
+    cap = cap ? cap : (1u << 20);
+    while (cap < want) cap *= 2;
+    return cap;
+  };
   if (bytes > c.h_cap) {
-    size_t cap = c.h_cap ? c.h_cap : (1u << 20);
-    while (cap < bytes) cap *= 2;
+    const size_t cap = grow(c.h_cap, bytes);
     if (c.h_buf) (void)hipHostFree(c.h_buf);
-    if (c.d_buf) (void)hipFree(c.d_buf);
     c.h_buf = nullptr;
-    c.d_buf = nullptr;
-    c.h_cap = c.d_cap = 0;
+    c.h_cap = 0;
     int rc = record_hip(hipHostMalloc((void**)&c.h_buf, cap, hipHostMallocMapped));
     if (rc) return rc;
-    rc = record_hip(hipMalloc((void**)&c.d_buf, cap));
+    c.h_cap = cap;
+  }
+  if (device && bytes > c.d_cap) {
+    const size_t cap = grow(c.d_cap, bytes);
+    if (c.d_buf) (void)hipFree(c.d_buf);
+    c.d_buf = nullptr;
+    c.d_cap = 0;
+    int rc = record_hip(hipMalloc((void**)&c.d_buf, cap));
     if (rc) return rc;
-    c.h_cap = c.d_cap = cap;
+    c.d_cap = cap;
   }
   if (nout > c.out_cap) {
     size_t cap = c.out_cap ? c.out_cap : 4096;
@@ -393,7 +411,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   using clk = std::chrono::steady_clock;
   const clk::time_point t0 = trace ? clk::now() : clk::time_point();
   double t_walk = 0, t_desc = 0;
-  int rc = ctx_reserve(c, std::max<size_t>(c.h_cap, 1u << 20), (size_t)n);
+  int rc = ctx_reserve(c, std::max<size_t>(c.h_cap, 1u << 20), (size_t)n, false);
   if (rc) return rc;
   uint64_t lo_addr = ~0ull;
   for (const Region& r : g_regions) lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
@@ -443,7 +461,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
       if (rc) return rc;
       ring = 0;
       if (need > c.h_cap) {
-        rc = ctx_reserve(c, need * (size_t)((nch - g0 + group - 1) / group), (size_t)n);
+        rc = ctx_reserve(c, need * (size_t)((nch - g0 + group - 1) / group), (size_t)n, false);
         if (rc) return rc;
         rc = record_hip(hipHostGetDevicePointer(&dbuf, c.h_buf, 0));
         if (rc) return rc;
@@ -568,9 +586,10 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
                    HeadFn head) {
   if (n < 0) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
-  Ctx& c = t_ctx;
-  int rc = ctx_ready(c);
+  Ctx* cp = nullptr;
+  int rc = ctx_current(&cp);
   if (rc) return rc;
+  Ctx& c = *cp;
 
   const int threads = tuning().host_threads;
   // ~16 chunks per thread: the staging path packs and ships them in groups
@@ -803,12 +822,6 @@ uint32_t in6_pseudo_fold(const uint8_t* ip6, uint32_t len, uint8_t nxt) {
   return fold16_host(s - in6_scope_word(ip6 + 8) - in6_scope_word(ip6 + 24));
 }
 
-[[noreturn]] void die(const char* fn, int rc) {
-  fprintf(stderr, "libuinet_cksum: %s failed: %s (hip error %d: %s)\n", fn,
-          uinet_cksum_strerror(rc), t_last_hip, hipGetErrorString((hipError_t)t_last_hip));
-  abort();
-}
-
 }  // namespace
 }  // namespace uinet
 
@@ -838,7 +851,7 @@ int uinet_cksum_register_host(void* base, size_t len) {
   for (const Region& r : g_regions)
     if (b < r.end && r.base < e) return UINET_CKSUM_EINVAL;  // overlaps
   bool owned = true;
-  hipError_t he = hipHostRegister(base, len, hipHostRegisterMapped);
+  hipError_t he = hipHostRegister(base, len, hipHostRegisterMapped | hipHostRegisterPortable);
   if (he == hipErrorHostMemoryAlreadyRegistered) {  // e.g. hipHostMalloc'd / torch-pinned
     (void)hipGetLastError();
     owned = false;
@@ -903,7 +916,7 @@ int uinet_cksum_spans(const void* base, const uint64_t* off, const uint32_t* len
 int uinet_cksum_strided(const void* base, uint64_t stride, uint32_t len, const uint32_t* seed,
                         uint16_t* out, uint32_t n, uint32_t flags, void* stream) {
   if (n == 0) return UINET_CKSUM_OK;
-  if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
+  if (n > UINET_CKSUM_MAX_PACKETS || len >= UINET_CKSUM_MAX_SPAN) return UINET_CKSUM_EINVAL;
   if (!base || !out) return UINET_CKSUM_EINVAL;
   return launch_strided(base, stride, len, seed, out, n, flags,
                         static_cast<hipStream_t>(stream));
@@ -988,35 +1001,29 @@ int in_cksum_hdr_batch(const struct ip* const* ip, unsigned int* out, int n) {
 }
 
 // ---- drop-in per-call ABI (sys/amd64/include/in_cksum.h:76-83) --------------
+//
+// One chain per call, folded on the calling thread (cksum_percall.cpp): a
+// synchronous GPU round trip per packet is ~30x slower than the fold, and
+// the reference has no error channel, so these never touch the device and
+// never fail.  Batches of packets go to the GPU (sections 2b-2d of the header).
 
 unsigned short in_cksum_skip(struct mbuf* m, int len, int skip) {
-  unsigned short r = 0;
-  const int rc = in_cksum_skip_batch(&m, &len, &skip, &r, 1);
-  if (rc) die("in_cksum_skip", rc);
-  return r;
+  return host_cksum_skip(reinterpret_cast<const MbufHdr*>(m), len, skip, 0u);
 }
 
 uint16_t in_cksum_pseudo_header(struct mbuf* m, int plen, int off0, uint32_t src, uint32_t dst,
                                 uint8_t protonum) {
-  uint16_t r = 0;
-  const int rc = in_cksum_pseudo_header_batch(&m, &plen, &off0, &src, &dst, &protonum, &r, 1);
-  if (rc) die("in_cksum_pseudo_header", rc);
-  return r;
+  return host_cksum_pseudo(reinterpret_cast<const MbufHdr*>(m), plen, off0, src, dst, protonum);
 }
 
-unsigned int in_cksum_hdr(const struct ip* ip) {
-  unsigned int r = 0;
-  const int rc = in_cksum_hdr_batch(&ip, &r, 1);
-  if (rc) die("in_cksum_hdr", rc);
-  return r;
-}
+unsigned int in_cksum_hdr(const struct ip* ip) { return host_cksum_hdr(ip); }
 
-// sys/netinet6/in6.h:638, in6_cksum.c:150-357.
+// sys/netinet6/in6.h:638, in6_cksum.c:150-357 (off counts from the chain
+// start, m_data at a contiguous IPv6 header).
 int in6_cksum(struct mbuf* m, uint8_t nxt, uint32_t off, uint32_t len) {
-  uint16_t r = 0;
-  const int rc = in6_cksum_batch(&m, &nxt, &off, &len, &r, 1);
-  if (rc) die("in6_cksum", rc);
-  return r;
+  const MbufHdr* mm = reinterpret_cast<const MbufHdr*>(m);
+  return host_cksum_skip(mm, (long)off + (long)len, (long)off,
+                         in6_pseudo_fold(mm->m_data, len, nxt));
 }
 
 // in6.h:637, in6_cksum.c:129-140: 36 header bytes, no payload -- a host fold.

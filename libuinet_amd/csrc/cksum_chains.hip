@@ -222,34 +222,41 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint32_t eff = hi > lo ? hi - lo : 0u;
       const uint64_t ao = so + lo;
       const uint32_t head = eff ? (uint32_t)(reinterpret_cast<uintptr_t>(base + ao) & 15) : 0u;
-      const uint32_t nch = eff ? (head + eff + 15) >> 4 : 0u;
+      // chunks touched, without forming head + eff (a u32 segment may be 4 GiB)
+      const uint32_t nch = eff ? (eff >> 4) + ((head + (eff & 15u) + 15u) >> 4) : 0u;
       const uint64_t c0 = ao - head;
       const uint32_t rot = ((pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(base + ao)) & 1u;
       const uint32_t meta = (slot << 1) | rot;
-      const uint32_t span = (eff << 4) | head;
       const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
       // --- long segments: one wave-wide span each -------------------------
       const bool is_long = nch >= kListMax || (long_ch != 0 && nch >= long_ch);
       for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
         const int s = (int)__builtin_ctzll(lm);
-        const uint32_t sp = __builtin_amdgcn_readlane(span, s);
+        // head and length read separately: a segment may hold up to 4 GiB,
+        // more than one packed 32-bit word (eff << 4 | head) keeps
+        const uint32_t h = __builtin_amdgcn_readlane(head, s);
+        const uint32_t el = __builtin_amdgcn_readlane(eff, s);
         const uint32_t mts = __builtin_amdgcn_readlane(meta, s);
         const uint8_t* cb = base + (((uint64_t)__builtin_amdgcn_readlane(c0_hi, s) << 32) |
                                     __builtin_amdgcn_readlane(c0_lo, s));
-        const int h = (int)(sp & 15), e = h + (int)(sp >> 4);
         const uint32_t nc = __builtin_amdgcn_readlane(nch, s);
+        // chunk k keeps bytes [k ? 0 : h, k < nc - 1 ? 16 : last_end): only the
+        // first and last chunks are partial, so no byte position is formed
+        const uint32_t last_end = ((h + (el & 15u) + 15u) & 15u) + 1u;
         uint64_t lsum = 0;
         for (uint32_t k0 = 0; k0 < nc; k0 += 64 * kLongU) {
           u32x4 v[kLongU];
 #pragma unroll
           for (int u = 0; u < kLongU; ++u)
             if (u == 0 || k0 + 64u * u < nc)
-              v[u] = load_chunk(cb + 16u * min(k0 + (uint32_t)(u * 64 + lane), nc - 1));
+              v[u] = load_chunk(cb + 16ull * min(k0 + (uint32_t)(u * 64 + lane), nc - 1));
 #pragma unroll
           for (int u = 0; u < kLongU; ++u) {
             if (u == 0 || k0 + 64u * u < nc) {
-              const int b = 16 * (int)(k0 + (uint32_t)(u * 64 + lane));
-              lsum += lut.sum(v[u], h - b, e - b);
+              const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
+              const int lo_b = k == 0 ? (int)h : (k < nc ? 0 : 16);
+              const int hi_b = k + 1 < nc ? 16 : (k + 1 == nc ? (int)last_end : 0);
+              lsum += lut.sum(v[u], lo_b, hi_b);
             }
           }
         }

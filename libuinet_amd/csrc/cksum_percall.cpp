@@ -1,0 +1,152 @@
+// The per-call drop-in ABI on the calling CPU thread:
+//   in_cksum_skip, in_cksum_pseudo_header, in_cksum_hdr, in6_cksum.
+//
+// Why the host: these symbols are called once per packet, synchronously, by
+// protocol code that holds one mbuf chain (ip_input.c:460-468 IP options,
+// ip_icmp.c, igmp.c, ip_fastfwd.c, timers; the hot RX/TX paths go through the
+// batch hooks).  A GPU round trip per call costs ~16 us against ~0.2 us of
+// folding 1500 bytes here, and the reference KPI has no error channel
+// (/root/reference/sys/amd64/amd64/in_cksum.c:193-285): these functions
+// must always return a sum, GPU or no GPU (SURVEY.md sections 7.3 and 8b).
+// The batch, device-resident and offload entry points are the GPU engine and
+// keep failing with UINET_CKSUM_ENODEV where there is no gfx950 device.
+//
+// Arithmetic.  A piece of the chain is summed as little-endian 64-bit words
+// loaded from ITS OWN start (unaligned loads, no read outside the piece), with
+// end-around carry; 2^64 = 1 (mod 65535), so the 64-bit one's-complement sum
+// is congruent to the 16-bit one and is zero only for all-zero bytes.  Byte k
+// of a piece then weighs 256^(k&1); a piece whose first byte sits at an odd
+// LOGICAL offset of the packet is byte-rotated once (x * 256 mod 65535) --
+// the reference reaches the same value by weighing with ADDRESS parity and
+// rotating when address and logical parity differ (:222-225).  The fold is
+// end-around carry (REDUCE16, :65-71), never "% 65535", so all-zero data
+// gives 0xffff and a sum of 0xffff gives 0.
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "host_batch.h"
+#include "uinet_cksum.h"
+
+namespace uinet {
+namespace {
+
+inline uint64_t add_eac(uint64_t a, uint64_t b) {
+  uint64_t s;
+  return __builtin_add_overflow(a, b, &s) ? s + 1 : s;  // s + 1 cannot wrap here
+}
+
+inline uint64_t load64(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+
+// 64-bit one's-complement sum of [p, p + n), byte k weighted 256^(k&1).
+uint64_t piece_sum(const uint8_t* p, size_t n) {
+  uint64_t a = 0, b = 0, c = 0, d = 0;  // four independent carry chains
+  while (n >= 32) {
+    a = add_eac(a, load64(p));
+    b = add_eac(b, load64(p + 8));
+    c = add_eac(c, load64(p + 16));
+    d = add_eac(d, load64(p + 24));
+    p += 32;
+    n -= 32;
+  }
+  while (n >= 8) {
+    a = add_eac(a, load64(p));
+    p += 8;
+    n -= 8;
+  }
+  if (n) {  // the last 1..7 bytes, zero-padded: byte k keeps weight 256^(k&1)
+    uint64_t t = 0;
+    memcpy(&t, p, n);
+    b = add_eac(b, t);
+  }
+  return add_eac(add_eac(a, b), add_eac(c, d));
+}
+
+inline uint32_t fold16(uint64_t s) {
+  s = (s & 0xffffffffull) + (s >> 32);
+  s = (s & 0xffff) + (s >> 16);
+  s = (s & 0xffff) + (s >> 16);
+  s = (s & 0xffff) + (s >> 16);
+  return (uint32_t)s;
+}
+
+inline uint32_t rot8(uint32_t x) { return ((x << 8) | (x >> 8)) & 0xffff; }
+
+inline uint16_t bswap16(uint16_t x) { return (uint16_t)((x << 8) | (x >> 8)); }
+
+// The reference chain walk (in_cksum.c:193-232, :241-276) summing as it goes.
+struct Walk {
+  uint64_t sum = 0;
+  long clen = 0;    // logical bytes consumed
+  long remain = 0;  // bytes still wanted
+
+  // in_cksum.c:219-228 / :263-272.  A negative mlen (len < skip, m_len <
+  // off0) is outside the reference's contract; it sums nothing here, and the
+  // length/parity bookkeeping follows the reference (the GPU batch path and
+  // the oracle do the same).
+  void take(const uint8_t* addr, long mlen) {
+    if (remain < mlen) mlen = remain;
+    if (mlen > 0) {
+      uint32_t x = fold16(piece_sum(addr, (size_t)mlen));
+      if (clen & 1) x = rot8(x);
+      sum += x;
+    }
+    clen += mlen;
+    remain -= mlen;
+  }
+  void take_rest(const MbufHdr* m) {  // in_cksum.c:214-229
+    for (; m && remain; m = m->m_next) {
+      if (m->m_len == 0) continue;
+      take(m->m_data, m->m_len);
+    }
+  }
+};
+
+inline uint16_t complement(uint64_t s) { return (uint16_t)(~fold16(s) & 0xffff); }
+
+}  // namespace
+
+// in_cksum.c:193-232 with `seed` added before the fold (0 for in_cksum_skip;
+// the folded IPv6 pseudo header for in6_cksum, in6_cksum.c:150-357).
+uint16_t host_cksum_skip(const MbufHdr* m, long len, long skip, uint32_t seed) {
+  Walk w;
+  w.sum = seed;
+  w.remain = len - skip;
+  while (skip && m) {  // in_cksum.c:203-212
+    if (m->m_len > skip) {
+      w.take(m->m_data + skip, (long)m->m_len - skip);
+      m = m->m_next;
+      skip = 0;
+      break;
+    }
+    skip -= m->m_len;
+    m = m->m_next;
+  }
+  if (skip == 0) w.take_rest(m);
+  return complement(w.sum);
+}
+
+uint16_t host_cksum_pseudo(const MbufHdr* m, int plen, int off0, uint32_t src, uint32_t dst,
+                           uint8_t proto) {
+  Walk w;
+  // in_cksum.c:252-253
+  w.sum = (uint64_t)src + dst + bswap16(proto) + bswap16((uint16_t)plen);
+  w.remain = plen;
+  w.take(m->m_data + off0, (long)m->m_len - off0);
+  w.take_rest(m->m_next);
+  return complement(w.sum);
+}
+
+// in_cksum.c:278-285: in_cksumdata(ip, 20) weighs bytes by ADDRESS parity and
+// never re-aligns, so a header at an odd address is the rotated sum.
+uint32_t host_cksum_hdr(const void* ip) {
+  uint32_t x = fold16(piece_sum(static_cast<const uint8_t*>(ip), 20));
+  if (reinterpret_cast<uintptr_t>(ip) & 1) x = rot8(x);
+  return complement(x);
+}
+
+}  // namespace uinet

@@ -57,4 +57,11 @@ struct Job {
 // launch).  Returns a UINET_CKSUM_* code.
 int run_jobs(const Job* jobs, int n, uint16_t* out);
 
+// The per-call ABI's host fold (cksum_percall.cpp): one chain on the calling
+// thread, no device involved, no error path (like the reference).
+uint16_t host_cksum_skip(const MbufHdr* m, long len, long skip, uint32_t seed);
+uint16_t host_cksum_pseudo(const MbufHdr* m, int plen, int off0, uint32_t src, uint32_t dst,
+                           uint8_t proto);
+uint32_t host_cksum_hdr(const void* ip);
+
 }  // namespace uinet
