@@ -60,7 +60,20 @@ uint64_t piece_sum(const uint8_t* p, size_t n) {
   }
   if (n) {  // the last 1..7 bytes, zero-padded: byte k keeps weight 256^(k&1)
     uint64_t t = 0;
-    memcpy(&t, p, n);
+    size_t k = 0;
+    if (n & 4) {
+      uint32_t v;
+      memcpy(&v, p, 4);
+      t = v;
+      k = 4;
+    }
+    if (n & 2) {
+      uint16_t v;
+      memcpy(&v, p + k, 2);
+      t |= (uint64_t)v << (8 * k);
+      k += 2;
+    }
+    if (n & 1) t |= (uint64_t)p[k] << (8 * k);
     b = add_eac(b, t);
   }
   return add_eac(add_eac(a, b), add_eac(c, d));
@@ -144,7 +157,10 @@ uint16_t host_cksum_pseudo(const MbufHdr* m, int plen, int off0, uint32_t src, u
 // in_cksum.c:278-285: in_cksumdata(ip, 20) weighs bytes by ADDRESS parity and
 // never re-aligns, so a header at an odd address is the rotated sum.
 uint32_t host_cksum_hdr(const void* ip) {
-  uint32_t x = fold16(piece_sum(static_cast<const uint8_t*>(ip), 20));
+  const uint8_t* p = static_cast<const uint8_t*>(ip);
+  uint32_t w;
+  memcpy(&w, p + 16, 4);
+  uint32_t x = fold16(add_eac(add_eac(load64(p), load64(p + 8)), w));
   if (reinterpret_cast<uintptr_t>(ip) & 1) x = rot8(x);
   return complement(x);
 }

@@ -181,6 +181,9 @@ class Reference:
             "refh_hdr_batch": (None, [_vp, _vp, _i32]),
             "refh_time_batch": (ctypes.c_double, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                                   _i32, _vp, _i32]),
+            "refh_in6_cksum": (_i32, [_vp, _u8, _u32, _u32]),
+            "refh_in6_cksum_pseudo": (_i32, [_vp, _u32, _u8, _u16]),
+            "refh_in6_batch": (None, [_vp, _vp, _vp, _vp, _vp, _i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -224,6 +227,20 @@ class Reference:
         ips = _c(ips, np.uint64)
         out = np.zeros(ips.size, np.uint32)
         self.L.refh_hdr_batch(_p(ips), _p(out), ips.size)
+        return out
+
+    def in6_cksum_pseudo(self, ip6: int, length: int, nxt: int, csum: int) -> int:
+        """sys/netinet6/in6_cksum.c:129-140, the reference's own."""
+        return self.L.refh_in6_cksum_pseudo(ip6, length, nxt, csum)
+
+    def in6_cksum_batch(self, heads, nxt, off, length) -> np.ndarray:
+        """in6_cksum(m, nxt, off, len) per packet, the reference's own
+        (in6_cksum.c:150-357; the chain must hold off + len bytes)."""
+        heads = _c(heads, np.uint64)
+        n = heads.size
+        arrs = [_c(nxt, np.uint8, n), _c(off, np.uint32, n), _c(length, np.uint32, n)]
+        out = np.zeros(n, np.uint16)
+        self.L.refh_in6_batch(_p(heads), *[_p(a) for a in arrs], _p(out), n)
         return out
 
     def time_skip(self, heads, length, skip, nthreads=1, cpus=None, reps=5):

@@ -15,6 +15,7 @@
 #include <pthread.h>
 #include <sched.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -58,6 +59,43 @@ unsigned short
 refh_in_addword(unsigned short a, unsigned short b)
 {
 	return ref_in_addword(a, b);
+}
+
+/* sys/netinet6/in6_cksum.c (renamed ref_*; see oracle/Makefile). */
+struct ip6_hdr;
+int ref_in6_cksum(struct mbuf *m, unsigned char nxt, unsigned off, unsigned len);
+int ref_in6_cksum_pseudo(struct ip6_hdr *ip6, unsigned len, unsigned char nxt,
+    unsigned short csum);
+
+/* The kernel's panic(), reached by in6_cksum only when the chain is shorter
+ * than off + len (in6_cksum.c:347); the tests never build such a chain. */
+void ref_panic(const char *fmt, ...) __attribute__((noreturn));
+void
+ref_panic(const char *fmt, ...)
+{
+	(void)fmt;
+	abort();
+}
+
+int
+refh_in6_cksum(struct mbuf *m, unsigned char nxt, unsigned off, unsigned len)
+{
+	return ref_in6_cksum(m, nxt, off, len);
+}
+
+int
+refh_in6_cksum_pseudo(struct ip6_hdr *ip6, unsigned len, unsigned char nxt,
+    unsigned short csum)
+{
+	return ref_in6_cksum_pseudo(ip6, len, nxt, csum);
+}
+
+void
+refh_in6_batch(struct mbuf *const *m, const unsigned char *nxt,
+    const unsigned *off, const unsigned *len, uint16_t *out, int n)
+{
+	for (int i = 0; i < n; i++)
+		out[i] = (uint16_t)ref_in6_cksum(m[i], nxt[i], off[i], len[i]);
 }
 
 void

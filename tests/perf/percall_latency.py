@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Latency of the per-call drop-in ABI (a GPU batch of one) and of host
-batches of various sizes, vs the reference object on the same host mbufs."""
-import json, os, sys, time
+"""Latency of the per-call drop-in ABI (a host fold on the calling thread)
+and of host batches of various sizes (GPU), vs the reference object on the
+same host mbufs.  The per-call numbers come twice: through ctypes, and from
+tests/perf/percall_bench.c (plain C, no interpreter in the loop)."""
+import json, os, subprocess, sys, tempfile, time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: F401  (one HIP runtime)
@@ -34,4 +36,15 @@ for nb in (64, 1024, 16384, 65536):
         t0 = time.perf_counter(); u.in_cksum_skip_batch(heads, 1500, 0); best = min(best, time.perf_counter() - t0)
     res[f"host_batch_{nb}_us"] = best * 1e6
     res[f"host_batch_{nb}_gibs"] = nb * 1500 / best / 2**30
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if R:
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "percall_bench")
+        lib, ref = os.path.join(REPO, "libuinet_amd"), os.path.join(REPO, "oracle", "_ref")
+        subprocess.run(["gcc", "-O2", "-std=c11", "-I", os.path.join(REPO, "include"),
+                        os.path.join(REPO, "tests", "perf", "percall_bench.c"), "-L", lib,
+                        "-luinet_cksum", f"-Wl,-rpath,{lib}", os.path.join(ref, "libref_cksum.so"),
+                        f"-Wl,-rpath,{ref}", "-o", exe], check=True)
+        res["c_percall"] = [json.loads(subprocess.run([exe, str(n)], capture_output=True, text=True,
+                                                      check=True).stdout) for n in (64, 1500, 9000)]
 print(json.dumps(res, indent=1))

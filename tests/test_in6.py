@@ -1,15 +1,15 @@
 """IPv6: in6_cksum / in6_cksum_pseudo / in6_cksum_batch.
 
 The reference's sys/netinet6/in6_cksum.c is not compiled by its own build
-(INET6 off) and cannot be built standalone here (it needs in6_getscope from
-scope6.c and the kernel's panic), so parity is pinned in two halves:
-  * the data walk -- the chain bytes [off, off + len) -- against the
-    reference object's own in_cksum_skip on the same chains;
-  * the pseudo header (in6_cksum.c:86-126: htonl(len), nxt, both addresses
-    minus their embedded scope zone) against a second, independent
-    restatement written here in Python;
-plus the self-verification property every receiver relies on: a segment
-whose checksum field holds in6_cksum's result sums to 0."""
+(INET6 off); oracle/Makefile compiles it with libuinet's kernel flags, plus
+the one function it calls from scope6.c (in6_getscope), into the reference
+object.  Parity is pinned to that object directly (in6_cksum and
+in6_cksum_pseudo on the same chains and headers, and the committed
+golden_in6.npz it generated, which the GPU box checks without the
+reference tree), and in two halves as before: the data walk against the
+reference's in_cksum_skip, the pseudo header against an independent Python
+restatement; plus the self-verification property every receiver relies on:
+a segment whose checksum field holds in6_cksum's result sums to 0."""
 from __future__ import annotations
 
 import numpy as np
@@ -48,7 +48,7 @@ def _addr(rng):
     return bytes(a)
 
 
-def build_ipv6(n: int, seed: int = 6):
+def build_ipv6(n: int, seed: int = 6, min_len: int = 0):
     """n IPv6 TCP/UDP/ICMPv6 packets; the first mbuf holds the whole IPv6
     header (in6_cksum's contract), the rest is cut into 0-300-B mbufs."""
     rng = np.random.default_rng(seed)
@@ -56,7 +56,7 @@ def build_ipv6(n: int, seed: int = 6):
     for _ in range(n):
         nxt = int(rng.choice([6, 17, 58]))
         ext = int(rng.choice([0, 0, 0, 8, 16]))   # extension headers before L4
-        plen = int(rng.integers(0, 1500))
+        plen = int(rng.integers(min_len, 1500))
         hdr = bytearray(40)
         hdr[0] = 0x60
         hdr[4:6] = (ext + plen).to_bytes(2, "big")
@@ -105,6 +105,63 @@ def test_in6_oracle_pinned(v6, ora, ref):
             s = (s & 0xFFFF) + (s >> 16)
         want.append(~s & 0xFFFF)
     np.testing.assert_array_equal(got, np.array(want, np.uint16))
+
+
+def test_in6_reference_pinned(ora, ref):
+    """The reference's own in6_cksum / in6_cksum_pseudo (in6_cksum.c:86-357)
+    against the oracle and the engine's per-call host fold.  Segments of at
+    least one byte: with len 0 and off at the very end of the chain the
+    reference dereferences the NULL m_next (in6_cksum.c:208-217), outside its
+    contract (a transport header is never empty)."""
+    import libuinet_amd as u
+
+    ch, nxt, off, ln, pkts = build_ipv6(1500, seed=9, min_len=1)
+    want = ref.in6_cksum_batch(ch.heads, nxt, off, ln)
+    np.testing.assert_array_equal(ora.in6_cksum_batch(ch.heads, nxt, off, ln), want)
+    got = [u.in6_cksum(int(ch.heads[i]), int(nxt[i]), int(off[i]), int(ln[i]))
+           for i in range(ch.n)]
+    np.testing.assert_array_equal(np.array(got, np.uint16), want)
+    rng = np.random.default_rng(3)
+    for i in range(0, ch.n, 5):
+        h = np.frombuffer(pkts[i][:40], np.uint8).copy()
+        length = int(rng.integers(0, 1 << 32))
+        csum = int(rng.integers(0, 1 << 16))
+        w = ref.in6_cksum_pseudo(h.ctypes.data, length, int(nxt[i]), csum)
+        assert ora.in6_cksum_pseudo(h.ctypes.data, length, int(nxt[i]), csum) == w
+        assert u.in6_cksum_pseudo(h.ctypes.data, length, int(nxt[i]), csum) == w
+
+
+def _golden_in6(golden):
+    g = golden("in6")
+    arena = aligned_empty(g["arena"].size)
+    arena[:] = g["arena"]
+    ch = MbufChains(arena, g["seg_off"], g["seg_len"], g["pkt_seg"])
+    return g, ch
+
+
+def test_in6_golden_per_call_and_oracle(golden, ora):
+    import libuinet_amd as u
+
+    g, ch = _golden_in6(golden)
+    np.testing.assert_array_equal(ora.in6_cksum_batch(ch.heads, g["nxt"], g["off"], g["len"]),
+                                  g["expected"])
+    for i in range(ch.n):
+        assert u.in6_cksum(int(ch.heads[i]), int(g["nxt"][i]), int(g["off"][i]),
+                           int(g["len"][i])) == g["expected"][i]
+    for i in range(g["p_hdr"].shape[0]):
+        h = np.ascontiguousarray(g["p_hdr"][i])
+        args = (h.ctypes.data, int(g["p_len"][i]), int(g["p_nxt"][i]), int(g["p_csum"][i]))
+        assert u.in6_cksum_pseudo(*args) == g["p_expected"][i]
+        assert ora.in6_cksum_pseudo(*args) == g["p_expected"][i]
+
+
+@pytest.mark.gpu
+def test_in6_golden_gpu(torch_dev, golden):
+    import libuinet_amd as u
+
+    g, ch = _golden_in6(golden)
+    np.testing.assert_array_equal(u.in6_cksum_batch(ch.heads, g["nxt"], g["off"], g["len"]),
+                                  g["expected"])
 
 
 def test_in6_pseudo_oracle_and_engine(v6, ora):
