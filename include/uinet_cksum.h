@@ -150,6 +150,9 @@ int uinet_cksum_device_ok(void);
  *                     1..64 (default min(16, hardware threads))
  *   "spans_contig"    span kernels: each block folds one contiguous packet
  *                     range (1) instead of grid-wide rounds (0, default)
+ *   "spans_geo"       span kernels: force the lanes-per-packet G and loads
+ *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
+ *                     16x3, 32x3, 64x2, 64x3); 0 = picked from len_hint
  *   "walk_prefetch"   host-mbuf batch walk: 0 = no prefetch, 1 = prefetch
  *                     mbuf headers a few packets ahead (default), 2 = chase
  *                     16 chains in lockstep (never changes results)
@@ -157,7 +160,8 @@ int uinet_cksum_device_ok(void);
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
  * (0|1, or serial), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
  * UINET_CKSUM_CHAINS_TILE, UINET_CKSUM_XCD_REMAP, UINET_CKSUM_SPANS_LUT,
- * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF and UINET_CKSUM_SPANS_CONTIG set
+ * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF, UINET_CKSUM_SPANS_CONTIG and
+ * UINET_CKSUM_SPANS_GEO set
  * the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 

@@ -125,6 +125,10 @@ int grid_for(uint32_t n, int g, int bpc) {
   return (int)blocks;
 }
 
+// Compiled geometries (G * 16 + U); the "spans_geo" knob forces one for A/B.
+// 16 x 6 and 8 x 12 (the 96 chunks of 32 x 3 with twice / four times the
+// bytes in flight per lane) needed 82 / 132 VGPRs and ran 2-3 % slower on
+// config 2 (profiles/r02/ab_geo/), so they are not built.
 #define UINET_DISPATCH_GEOMETRY(GEO, LAUNCH)          \
   switch ((GEO).g * 16 + (GEO).u) {                   \
     case 4 * 16 + 1: LAUNCH(4, 1); break;             \
@@ -138,6 +142,21 @@ int grid_for(uint32_t n, int g, int bpc) {
   }
 
 }  // namespace
+
+bool span_geometry_ok(int code) {
+  switch (code) {
+    case 4 * 16 + 1: case 4 * 16 + 2: case 8 * 16 + 1: case 8 * 16 + 2: case 16 * 16 + 3:
+    case 32 * 16 + 3: case 64 * 16 + 2: case 64 * 16 + 3:
+      return true;
+    default:
+      return false;
+  }
+}
+
+static Geometry geometry_override(Geometry g) {
+  const int v = tuning().spans_geo;
+  return v ? Geometry{v / 16, v % 16} : g;
+}
 
 // Blocks per CU.  Measured on MI355X by interleaved A/B (config 2,
 // profiles/r01/ab/): the span kernel peaks at 256 (2 packets per group --
@@ -154,7 +173,7 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
                  const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                  uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
-  const Geometry geo = pick_geometry(len_hint);
+  const Geometry geo = geometry_override(pick_geometry(len_hint));
   const int grid = grid_for(n, geo.g, 256);
 #define L(G, U)                                                                          \
   if (tuning().spans_lut)                                                                \
@@ -178,6 +197,7 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   Geometry geo = pick_geometry(len);
   // 16-B aligned packets of at most 64 B hold at most 4 chunks: one per lane
   if (len <= 64 && ((reinterpret_cast<uintptr_t>(base) | pkt_stride) & 15) == 0) geo = {4, 1};
+  geo = geometry_override(geo);
   // one packet per group suits long packets; small ones want groups that
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
   const int grid = grid_for(n, geo.g, len <= 96 ? 256 : 4096);
