@@ -57,7 +57,10 @@ def main():
         if R is not None:
             t1, r1 = R.time_skip(ch.heads, ln, sk, nthreads=1, reps=3)
             e["reference_1thread_gibs"] = round(gib / t1, 2)
-            e["equal_reference"] = bool(np.array_equal(r1, r_zc))
+            cpus = sorted(os.sched_getaffinity(0))[:16]
+            t16, r16 = R.time_skip(ch.heads, ln, sk, nthreads=len(cpus), cpus=cpus, reps=5)
+            e[f"reference_{len(cpus)}thread_gibs"] = round(gib / t16, 2)
+            e["equal_reference"] = bool(np.array_equal(r1, r_zc) and np.array_equal(r16, r_zc))
         res[name] = e
         print(name, e, flush=True)
     print(json.dumps(res))

@@ -106,8 +106,32 @@ def main():
                                                    proto)), a.reps)
         res["reference_1thread_tx_ms"] = round(t_tx * 1e3, 3)
         res["reference_1thread_rx_ms"] = round(t_rx * 1e3, 3)
+        # the same calls split over the box's host threads (ctypes releases the
+        # GIL, so the slices run in parallel on up to 16 cores)
+        from concurrent.futures import ThreadPoolExecutor
+        nt = min(16, len(os.sched_getaffinity(0)))
+        pool = ThreadPoolExecutor(nt)
+
+        def par(fn, idx):
+            return list(pool.map(fn, np.array_split(idx, nt)))
+
+        t_tx16 = best(lambda: (par(lambda k: R.skip_batch(ref_fb.tx.heads[l4][k], txl[k], txs[k]),
+                                   np.arange(l4.size)),
+                               par(lambda k: R.skip_batch(ref_fb.tx.heads[ipd][k],
+                                                          (fb.l3 + fb.hlen)[ipd][k], fb.l3[ipd][k]),
+                                   np.arange(ipd.size))), a.reps)
+        plen4 = (ip_len - fb.hlen)[l4]
+        off4 = (fb.l3 + fb.hlen)[l4]
+        t_rx16 = best(lambda: (par(lambda k: R.hdr_batch(ips[k]), np.arange(ips.size)),
+                               par(lambda k: R.pseudo_header_batch(rx_o.heads[l4][k], plen4[k], off4[k],
+                                                                   fb.src[l4][k], fb.dst[l4][k],
+                                                                   proto[k]), np.arange(l4.size))),
+                      a.reps)
+        pool.shutdown()
+        res[f"reference_{nt}thread_tx_ms"] = round(t_tx16 * 1e3, 3)
+        res[f"reference_{nt}thread_rx_ms"] = round(t_rx16 * 1e3, 3)
     for k in ("tx_staged", "tx_zero_copy", "rx_staged", "rx_zero_copy", "reference_1thread_tx",
-              "reference_1thread_rx"):
+              "reference_1thread_rx", "reference_16thread_tx", "reference_16thread_rx"):
         if f"{k}_ms" in res:
             res[f"{k}_gibs"] = round(nbytes / (res[f"{k}_ms"] * 1e-3) / 2**30, 2)
     print(json.dumps(res), flush=True)
