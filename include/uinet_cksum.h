@@ -150,6 +150,9 @@ int uinet_cksum_device_ok(void);
  *                     1..64 (default min(16, hardware threads))
  *   "spans_contig"    span kernels: each block folds one contiguous packet
  *                     range (1) instead of grid-wide rounds (0, default)
+ *   "spans_sdesc"     span kernels with 32 or 64 lanes per packet: load the
+ *                     wave's packet descriptors with scalar loads (1, default)
+ *                     or one vector load per lane group (0)
  *   "spans_geo"       span kernels: force the lanes-per-packet G and loads
  *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
  *                     16x3, 32x3, 64x2, 64x3); 0 = picked from len_hint
@@ -160,8 +163,8 @@ int uinet_cksum_device_ok(void);
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
  * (0|1, or serial), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
  * UINET_CKSUM_CHAINS_TILE, UINET_CKSUM_XCD_REMAP, UINET_CKSUM_SPANS_LUT,
- * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF, UINET_CKSUM_SPANS_CONTIG and
- * UINET_CKSUM_SPANS_GEO set
+ * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF, UINET_CKSUM_SPANS_CONTIG,
+ * UINET_CKSUM_SPANS_GEO and UINET_CKSUM_SPANS_SDESC set
  * the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 

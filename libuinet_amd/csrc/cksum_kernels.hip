@@ -28,7 +28,47 @@
 namespace uinet {
 namespace {
 
-template <int G, int U, bool kStrided, bool kLut>
+// Scalar (SMEM) loads of words the kernel never writes: through the constant
+// address space a uniform load becomes an s_load, served by the scalar cache
+// instead of the vector memory pipeline that streams the packet bytes.
+__device__ __forceinline__ uint64_t sload64(const uint64_t* p) {
+  return *(const __attribute__((address_space(4))) uint64_t*)(uintptr_t)p;
+}
+__device__ __forceinline__ uint32_t sload32(const uint32_t* p) {
+  return *(const __attribute__((address_space(4))) uint32_t*)(uintptr_t)p;
+}
+
+// The descriptors of packet p for lane group `gi` of a wave whose kP = 64 / G
+// groups own the consecutive packets p - gi .. p - gi + kP - 1: kP scalar
+// loads of off / len (clamped to n - 1), then a per-lane select.  Without
+// it every group's off[p] / len[p] is a vector load of its own, 2 of the 5
+// vector-memory instructions per wave and packet pair at 1500 B.
+template <int G>
+__device__ __forceinline__ void wave_desc(const uint64_t* __restrict__ off,
+                                          const uint32_t* __restrict__ len, uint32_t p, uint32_t n,
+                                          uint64_t& o, uint32_t& l) {
+  constexpr int kP = 64 / G;
+  const uint32_t gi = (threadIdx.x & 63) / G;
+  const uint32_t p0 = __builtin_amdgcn_readfirstlane(p - gi);
+  o = 0;
+  l = 0;
+#pragma unroll
+  for (int k = 0; k < kP; ++k) {
+    const uint32_t q = min(p0 + (uint32_t)k, n - 1);
+    // readfirstlane keeps each value scalar: without it the compiler folds
+    // the select of kP loads back into one per-lane (vector) load of off[p]
+    const uint64_t o64 = sload64(off + q);
+    const uint64_t ok = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o64 >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)o64);
+    const uint32_t lk = __builtin_amdgcn_readfirstlane(sload32(len + q));
+    if (gi == (uint32_t)k) {
+      o = ok;
+      l = lk;
+    }
+  }
+}
+
+template <int G, int U, bool kStrided, bool kLut, bool kSDesc = false>
 __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ base,
                                                  const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ len,
@@ -59,7 +99,10 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
   const bool live = p < pend;
   uint64_t o = 0;
   uint32_t l = 0;
-  if (live) {
+  if constexpr (kSDesc && !kStrided) {
+    wave_desc<G>(off, len, p, n, o, l);
+    if (!live) l = 0;
+  } else if (live) {
     o = kStrided ? (uint64_t)p * pkt_stride : off[p];
     l = kStrided ? fixed_len : len[p];
   }
@@ -74,8 +117,14 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
     // prefetch the next packet's descriptors behind this packet's loads
     const uint32_t pn = p + stride;
     const uint32_t pc = min(pn, n - 1);
-    const uint64_t on = kStrided ? (uint64_t)pc * pkt_stride : off[pc];
-    const uint32_t ln = kStrided ? fixed_len : len[pc];
+    uint64_t on;
+    uint32_t ln;
+    if constexpr (kSDesc && !kStrided) {
+      wave_desc<G>(off, len, pn, n, on, ln);
+    } else {
+      on = kStrided ? (uint64_t)pc * pkt_stride : off[pc];
+      ln = kStrided ? fixed_len : len[pc];
+    }
     uint64_t acc;
     if (kLut) {
       acc = l ? sp.sum_lut(lut, 0, gl) : 0;
@@ -174,9 +223,21 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
                  uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = geometry_override(pick_geometry(len_hint));
-  const int grid = grid_for(n, geo.g, 256);
+  // Scalar descriptors (G >= 32, knob "spans_sdesc", default on): a wave's
+  // 1-2 packets' off / len come from s_loads, and the grid drops to one packet
+  // per group (512 blocks per CU at 1 M x 1500 B).  Interleaved A/B, config 2
+  // (profiles/r02/ab_sdesc/): vector descriptors at 256 / CU 0.2192 ms,
+  // scalar at 256 / CU 0.2167, scalar at 512 / CU 0.2086 (+5.1 %), 4096 / CU
+  // 0.2095; on a slower stretch of the same box +1.4 %.
+  const bool sdesc = tuning().spans_sdesc && geo.g >= 32;
+  const int grid = grid_for(n, geo.g, sdesc ? 512 : 256);
 #define L(G, U)                                                                          \
-  if (tuning().spans_lut)                                                                \
+  if (sdesc && (G) >= 32)                                                                \
+    hipLaunchKernelGGL((k_spans<G, U, false, true, true>), dim3(grid), dim3(kBlock), 0,  \
+                       stream, static_cast<const uint8_t*>(base), off, len, seed, parity, \
+                       0ull, 0u, out, n, flags, (uint32_t)tuning().xcd_remap,            \
+                       (uint32_t)tuning().spans_contig);                                 \
+  else if (tuning().spans_lut)                                                           \
     hipLaunchKernelGGL((k_spans<G, U, false, true>), dim3(grid), dim3(kBlock), 0, stream, \
                        static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
                        out, n, flags, (uint32_t)tuning().xcd_remap,                      \
