@@ -361,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_grp(const uint8_t* __restrict__ base
 // k_chains_pipe with ablations: 1 = no chunk arithmetic / binning (bytes
 // xor-ed into a register), 2 = no loads, 3 = chunk sums but no binning.
 template <int kAbl, int kPass, int kTile, typename OffT, typename LenT>
-__global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_pipe_abl(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UINET_CHAINS_OCC void k_pipe_abl(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
                                                        const LenT* __restrict__ seg_len,
                                                        const uint32_t* __restrict__ pkt_seg,
@@ -403,6 +403,8 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_pipe_abl(const uint
       const uint32_t w = lut.sum_oc_idx(v[q], key[q] & 0xffffu);  // < 2^17
       if constexpr (kAbl == 3) { dummy += w; continue; }
       const uint32_t sl = key[q] >> 16;
+      if constexpr (kAbl == 6) { atomicAdd(&acc[sl], (unsigned long long)w); continue; }
+      if constexpr (kAbl == 7) { atomicAdd(reinterpret_cast<uint32_t*>(&acc[sl]), w); continue; }
       const uint32_t P = wave_scan<0, false>(w, 0u);  // < 2^23
       const uint32_t nx = wave_shl1(sl);
       if (lane == 63 || nx != sl) {
@@ -658,6 +660,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
       const uint32_t w = lut.sum_oc_idx(v[q], key[q] & 0xffffu);  // < 2^17
       if constexpr (kAbl == 3) { dummy += w; continue; }
       const uint32_t sl = key[q] >> 16;
+      if constexpr (kAbl == 6) { atomicAdd(&acc[sl], (unsigned long long)w); continue; }
+      if constexpr (kAbl == 7) { atomicAdd(reinterpret_cast<uint32_t*>(&acc[sl]), w); continue; }
       const uint32_t P = wave_scan<0, false>(w, 0u);  // < 2^23
       const uint32_t nx = wave_shl1(sl);
       if (lane == 63 || nx != sl) {
@@ -1012,6 +1016,9 @@ int main(int argc, char** argv) {
   ADD("pingpong P2", true, hipLaunchKernelGGL((lab::k_pipe_abl<4, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   ADD("pingpong P1", true, hipLaunchKernelGGL((lab::k_pipe_abl<4, 1, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   ADD("pingpong P3", true, hipLaunchKernelGGL((lab::k_pipe_abl<4, 3, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
+  // lab6: per-chunk LDS atomics instead of the telescoping scan (u64 / low u32 word)
+  ADD("direct atomics u64", true, hipLaunchKernelGGL((lab::k_pipe_abl<6, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
+  ADD("direct atomics u32", false, hipLaunchKernelGGL((lab::k_pipe_abl<7, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   // lab4: G lanes per segment
   ADD("grp<8,2>", true, hipLaunchKernelGGL((lab::k_grp<8, 2, 32>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   ADD("grp<4,4>", true, hipLaunchKernelGGL((lab::k_grp<4, 4, 32>), dim3(grid_for_tiles(d.n, 32)), KARGS))
