@@ -258,11 +258,12 @@ int uinet_cksum_unregister_host(void *base);
 /* ------------------------------------------------------------------------ */
 /* 2d. Driver batch offload            */
 /*                                                                          */
-/* Whole RX / TX batches of IPv4 packets, each one mbuf chain with          */
+/* Whole RX / TX batches of IPv4 and IPv6 packets, each one mbuf chain with */
 /* M_PKTHDR set.  `l2len` is the byte offset of the IP header from m_data:  */
-/* -1 = parse an Ethernet header (14 bytes, 18 with one 802.1Q tag), 0 =    */
-/* m_data points at the IP header (ip_output's view).  One GPU batch per    */
-/* call; status[i] (may be NULL) receives UINET_RX_* / UINET_TX_* bits.     */
+/* -1 = parse an Ethernet header (14 bytes, 18 with one 802.1Q tag; type    */
+/* 0x0800 or 0x86dd), >= 0 = the IP header is there and its version nibble  */
+/* tells IPv4 from IPv6 (ip_output's view: 0).  One GPU batch per call;     */
+/* status[i] (may be NULL) receives UINET_RX_* / UINET_TX_* bits.           */
 /* ------------------------------------------------------------------------ */
 
 #define UINET_RX_IPV4    0x01 /* IPv4 header parsed */
@@ -271,6 +272,7 @@ int uinet_cksum_unregister_host(void *base);
 #define UINET_RX_L4_OK   0x08 /* ... and it verifies */
 #define UINET_RX_NOSUM   0x10 /* UDP datagram without checksum (uh_sum 0) */
 #define UINET_RX_FRAG    0x20 /* fragment: L4 left to the stack after reassembly */
+#define UINET_RX_IPV6    0x40 /* IPv6 header parsed (no header checksum) */
 
 /* RX (first-look hook / uinet_pd_deliver_to_stack, uinet_api.c:2165-2187):
  * verifies every packet's IPv4 header and TCP/UDP checksum and records the
@@ -282,20 +284,34 @@ int uinet_cksum_unregister_host(void *base);
  *   CSUM_PSEUDO_HDR, csum_data = in_cksum_pseudo_header(...) ^ 0xffff
  *   (0xffff for a good packet, as if_loop.c:96-101 sets it).
  * UDP covers uh_ulen bytes (udp_usrreq.c:404-412); fragments, truncated
- * chains and non-IPv4 frames get no L4 marks. */
+ * chains and non-IP frames get no L4 marks.
+ * IPv6 (UINET_RX_IPV6): TCP or UDP directly after the fixed header gets the
+ * same CSUM_DATA_VALID_IPV6 | CSUM_PSEUDO_HDR marks over the IPv6 pseudo
+ * header (in6_cksum.c:86-126), read back by tcp_input.c:627-639 and
+ * udp6_usrreq.c:233-246.  No marks for: extension headers (fragments set
+ * UINET_RX_FRAG), jumbograms (ip6_plen 0), truncated chains, UDP whose
+ * uh_ulen differs from ip6_plen (udps_badlen) or whose uh_sum is 0
+ * (UINET_RX_NOSUM; an error in IPv6), and link-local / interface-local
+ * addresses carrying a zone word, which ip6_input.c:658-661 drops. */
 int uinet_cksum_rx_offload(struct mbuf *const *m, int n, int l2len,
     uint8_t *status);
 
 #define UINET_TX_L4      0x01 /* th_sum / uh_sum computed and stored */
 #define UINET_TX_IP      0x02 /* ip_sum computed and stored */
 #define UINET_TX_L4_LOST 0x04 /* checksum field beyond the first mbuf: not stored */
-#define UINET_TX_SKIP    0x08 /* no M_PKTHDR, not IPv4, or CSUM_TSO */
+#define UINET_TX_SKIP    0x08 /* no M_PKTHDR, not IP, nothing asked, or CSUM_TSO */
+#define UINET_TX_IPV6    0x10 /* an IPv6 packet (with UINET_TX_L4 or _L4_LOST) */
 
 /* TX (if_netmap_batch_send, uinet_if_netmap.c:1196-1262, with if_hwassist =
  * CSUM_IP|CSUM_TCP|CSUM_UDP so ip_output defers, ip_output.c:645-656): for
  * every packet whose csum_flags ask for it, does what in_delayed_cksum
  * (ip_output.c:953-976, the in_pseudo seed already in th_sum) and the
- * ip_sum store (:665-667) do, then clears those csum_flags bits. */
+ * ip_sum store (:665-667) do, then clears those csum_flags bits.
+ * IPv6 (if_hwassist also CSUM_TCP_IPV6|CSUM_UDP_IPV6 0x4000|0x2000, so
+ * ip6_output.c:966-988 defers): in6_delayed_cksum (ip6_output.c:188-209),
+ * in_cksum_skip(m, 40 + ip6_plen, 40) over the in6_cksum_pseudo seed that
+ * tcp_output.c:1069-1071 / udp6_usrreq.c:786 stored, UDP 0 -> 0xffff,
+ * stored at 40 + csum_data; jumbograms (ip6_plen 0) are skipped. */
 int uinet_cksum_tx_offload(struct mbuf *const *m, int n, int l2len,
     uint8_t *status);
 

@@ -1,13 +1,19 @@
-// Driver batch offload: whole RX / TX batches of
-// IPv4 packets checksummed in one GPU batch, with the results recorded the
-// way the stack consumes a checksum-offloading NIC's work.
+// Driver batch offload (SURVEY.md 8f items 1-2, IPv6 with item 4): whole RX /
+// TX batches of IPv4 and IPv6 packets checksummed in one GPU batch, with the
+// results recorded the way the stack consumes a checksum-offloading NIC's
+// work.
 //
 //   RX  ip_input.c:460-471 (CSUM_IP_CHECKED / CSUM_IP_VALID),
 //       tcp_input.c:697-718 and udp_usrreq.c:428-449 (CSUM_DATA_VALID |
-//       CSUM_PSEUDO_HDR: th_sum = csum_data ^ 0xffff must be 0).
+//       CSUM_PSEUDO_HDR: th_sum = csum_data ^ 0xffff must be 0);
+//       IPv6: tcp_input.c:627-639 and udp6_usrreq.c:216-246 read the same
+//       marks (CSUM_DATA_VALID_IPV6 == CSUM_DATA_VALID, mbuf.h:302).
 //   TX  ip_output.c:645-667 (deferred ip_sum) and :953-976 (in_delayed_cksum:
 //       in_cksum_skip(m, ip_len, hlen) over the in_pseudo seed already in
-//       th_sum, UDP 0 -> 0xffff, stored at hlen + csum_data).
+//       th_sum, UDP 0 -> 0xffff, stored at hlen + csum_data);
+//       IPv6: ip6_output.c:966-988 and :188-209 (in6_delayed_cksum:
+//       in_cksum_skip(m, 40 + plen, 40) over the in6_cksum_pseudo seed that
+//       tcp_output.c:1069-1071 / udp6_usrreq.c:786 put in the checksum field).
 //
 // The host parses headers (a few bytes per packet, already in cache from the
 // driver) and writes flags; every byte sum is a GPU job (host_batch.h).
@@ -26,6 +32,7 @@ namespace {
 // sys/sys/mbuf.h:182,281-293; sys/netinet/ip.h:63-65.
 constexpr int kMPktHdr = 0x2;
 constexpr int kCsumIp = 0x1, kCsumTcp = 0x2, kCsumUdp = 0x4, kCsumTso = 0x20;
+constexpr int kCsumUdpIpv6 = 0x2000, kCsumTcpIpv6 = 0x4000;  // mbuf.h:295-296
 constexpr int kCsumIpChecked = 0x100, kCsumIpValid = 0x200, kCsumDataValid = 0x400,
               kCsumPseudoHdr = 0x800;
 constexpr int kIpMf = 0x2000, kIpOffMask = 0x1fff;
@@ -68,22 +75,30 @@ struct Ip4 {
   int l4_have = 0;
 };
 
-// l2len -1: Ethernet (0x0800, or one 802.1Q tag then 0x0800).
-bool parse_ip4(const MbufHdr* m, int l2len, Ip4* o) {
-  uint8_t b[18 + 60 + 8];
-  int l3 = l2len;
-  if (l2len < 0) {
-    const int got = chain_read(m, 0, b, 18);
-    if (got < 14) return false;
-    uint16_t et = be16(b + 12);
-    l3 = 14;
-    if (et == 0x8100) {
-      if (got < 18) return false;
-      et = be16(b + 16);
-      l3 = 18;
-    }
-    if (et != 0x0800) return false;
+// The network header's offset and IP version (4 or 6; 0 = neither).
+// l2len -1: Ethernet (0x0800 / 0x86dd, or one 802.1Q tag first); l2len >= 0:
+// the header sits at l2len and its version nibble tells.
+int l3_locate(const MbufHdr* m, int l2len, int* l3) {
+  uint8_t b[18];
+  if (l2len >= 0) {
+    *l3 = l2len;
+    if (chain_read(m, l2len, b, 1) < 1) return 0;
+    return (b[0] >> 4) == 4 ? 4 : (b[0] >> 4) == 6 ? 6 : 0;
   }
+  const int got = chain_read(m, 0, b, 18);
+  if (got < 14) return 0;
+  uint16_t et = be16(b + 12);
+  *l3 = 14;
+  if (et == 0x8100) {
+    if (got < 18) return 0;
+    et = be16(b + 16);
+    *l3 = 18;
+  }
+  return et == 0x0800 ? 4 : et == 0x86dd ? 6 : 0;
+}
+
+bool parse_ip4(const MbufHdr* m, int l3, Ip4* o) {
+  uint8_t b[60 + 8];
   const int got = chain_read(m, l3, b, 60 + 8);
   if (got < 20 || (b[0] >> 4) != 4) return false;
   const int hl = (b[0] & 15) * 4;
@@ -105,6 +120,50 @@ uint32_t fold16(uint64_t s) {
   return (uint32_t)s;
 }
 
+// The fixed IPv6 header and the first 8 bytes after it.  Extension headers
+// are not walked: a packet whose ip6_nxt is not TCP or UDP gets no L4 job.
+struct Ip6 {
+  int l3 = 0;
+  int plen = 0;  // ip6_plen
+  int nxt = 0;
+  uint8_t addr[32] = {};  // source, destination
+  uint8_t l4[8] = {};
+  int l4_have = 0;
+};
+
+bool parse_ip6(const MbufHdr* m, int l3, Ip6* o) {
+  uint8_t b[40 + 8];
+  const int got = chain_read(m, l3, b, 40 + 8);
+  if (got < 40 || (b[0] >> 4) != 6) return false;
+  o->l3 = l3;
+  o->plen = be16(b + 4);
+  o->nxt = b[6];
+  memcpy(o->addr, b + 8, 32);
+  o->l4_have = got - 40;
+  memcpy(o->l4, b + 40, (size_t)o->l4_have);
+  return true;
+}
+
+// A link-local unicast, or link- / interface-local multicast, address whose
+// second 16-bit word (KAME's embedded zone) is nonzero.  ip6_input drops such
+// packets before any transport input (ip6_input.c:658-661, "badscope"), so
+// the RX hook leaves them unmarked.
+bool ip6_zone_embedded(const uint8_t* a) {
+  const bool ll = a[0] == 0xfe && (a[1] & 0xc0) == 0x80;
+  const bool mc = a[0] == 0xff && ((a[1] & 0x0f) == 0x02 || (a[1] & 0x0f) == 0x01);
+  return (ll || mc) && (a[2] | a[3]) != 0;
+}
+
+// in6_cksum.c:86-126 for wire addresses (no embedded zone): htonl(len),
+// three zero bytes and nxt, then both addresses, as little-endian 16-bit
+// words; folded so it fits a job seed.
+uint32_t pseudo6_seed(const Ip6& ip, uint32_t len) {
+  uint64_t s = (uint64_t)bswap16((uint16_t)(len >> 16)) + bswap16((uint16_t)len) +
+               bswap16((uint16_t)ip.nxt);
+  for (int i = 0; i < 32; i += 2) s += (uint64_t)(ip.addr[i] | ip.addr[i + 1] << 8);
+  return fold16(s);
+}
+
 // in_cksum.c:252-253, folded so it fits a job seed.
 uint32_t pseudo_seed(uint32_t src, uint32_t dst, int proto, int plen) {
   return fold16((uint64_t)src + dst + bswap16((uint16_t)proto) + bswap16((uint16_t)plen));
@@ -119,12 +178,34 @@ struct RxPlan {
 };
 
 struct TxPlan {
-  Ip4 ip;
+  int ip_l3 = 0;  // chain offset of the IPv4 header (ip_sum at +10)
   bool ip_job = false, l4_job = false;
   int l4_store = 0;  // chain offset of th_sum / uh_sum
   bool udp = false;
+  int clear = 0;  // csum_flags bits the hook takes over
   uint8_t st = 0;
 };
+
+// RX IPv6: tcp_input.c:627-639 (tlen = ip6_plen for a bare header) and
+// udp6_usrreq.c:216-246 (uh_ulen must equal the payload length, uh_sum 0 is
+// an error).  Returns the L4 job, or m == nullptr for none.
+Job rx6_job(const MbufHdr* m, const Ip6& ip, uint8_t* st) {
+  const Job none{nullptr, 0, 0, 0u};
+  if (ip.nxt == 44) *st |= UINET_RX_FRAG;
+  if (ip.plen == 0 || chain_len(m) < (long)ip.l3 + 40 + ip.plen) return none;  // jumbo, short
+  if (ip6_zone_embedded(ip.addr) || ip6_zone_embedded(ip.addr + 16)) return none;
+  if (ip.nxt == 17) {
+    if (ip.l4_have < 8) return none;
+    if (be16(ip.l4 + 4) != ip.plen) return none;  // udps_badlen
+    if (be16(ip.l4 + 6) == 0) {                    // udps_nosum
+      *st |= UINET_RX_NOSUM;
+      return none;
+    }
+  } else if (ip.nxt != 6) {
+    return none;
+  }
+  return Job{m, ip.l3 + 40 + ip.plen, ip.l3 + 40, pseudo6_seed(ip, (uint32_t)ip.plen)};
+}
 
 thread_local std::vector<Job> t_jobs;
 thread_local std::vector<uint16_t> t_res;
@@ -159,7 +240,20 @@ int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
     for (int i = i0; i < i1; i++) {
       const MbufHdr* m = reinterpret_cast<const MbufHdr*>(mv[i]);
       RxPlan& p = plan[(size_t)i];
-      if (!m || !parse_ip4(m, l2len, &p.ip)) continue;
+      int l3 = 0;
+      const int ver = m ? l3_locate(m, l2len, &l3) : 0;
+      if (ver == 6) {
+        Ip6 ip6;
+        if (!parse_ip6(m, l3, &ip6)) continue;
+        p.st |= UINET_RX_IPV6;
+        const Job j = rx6_job(m, ip6, &p.st);
+        if (j.m) {
+          p.l4_job = true;
+          jobs[2 * (size_t)i + 1] = j;
+        }
+        continue;
+      }
+      if (ver != 4 || !parse_ip4(m, l3, &p.ip)) continue;
       const Ip4& ip = p.ip;
       p.st |= UINET_RX_IPV4;
       p.ip_job = true;  // in_cksum(m, hlen) over the header (ip_input.c:463-467)
@@ -233,18 +327,34 @@ int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
         continue;
       }
       const int fl = pkthdr_of(m)->csum_flags;
-      if ((fl & kCsumTso) || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) ||
-          !parse_ip4(m, l2len, &p.ip)) {
+      int l3 = 0;
+      const int ver = (fl & kCsumTso) ? 0 : l3_locate(m, l2len, &l3);
+      if (ver == 6) {  // in6_delayed_cksum, ip6_output.c:188-209,978-981
+        Ip6 ip6;
+        if (!(fl & (kCsumTcpIpv6 | kCsumUdpIpv6)) || !parse_ip6(m, l3, &ip6) || ip6.plen == 0) {
+          p.st = UINET_TX_SKIP;
+          continue;
+        }
+        p.st = UINET_TX_IPV6;
+        p.udp = (fl & kCsumUdpIpv6) != 0;
+        p.clear = kCsumTcpIpv6 | kCsumUdpIpv6;
+        p.l4_store = l3 + 40 + pkthdr_of(m)->csum_data;
+        p.l4_job = true;
+        jobs[2 * (size_t)i + 1] = {m, l3 + 40 + ip6.plen, l3 + 40, 0u};
+        continue;
+      }
+      Ip4 ip;
+      if (ver != 4 || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) || !parse_ip4(m, l3, &ip)) {
         p.st = UINET_TX_SKIP;
         continue;
       }
-      const Ip4& ip = p.ip;
       if ((fl & kCsumIp) && ip.l3 + 12 > m->m_len) {
         p.st = UINET_TX_SKIP;  // header not in the first mbuf: leave it to the stack
         continue;
       }
       if (fl & (kCsumTcp | kCsumUdp)) {  // in_delayed_cksum, ip_output.c:958-963
         p.udp = (fl & kCsumUdp) != 0;
+        p.clear = kCsumTcp | kCsumUdp;
         p.l4_store = ip.l3 + ip.hl + pkthdr_of(m)->csum_data;
         p.l4_job = true;
         jobs[2 * (size_t)i + 1] = {m, ip.l3 + ip.ip_len, ip.l3 + ip.hl, 0u};
@@ -252,6 +362,7 @@ int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
       if (fl & kCsumIp) {  // ip_output.c:665-667: ip_sum = 0, then in_cksum(m, hlen)
         m->m_data[ip.l3 + 10] = 0;
         m->m_data[ip.l3 + 11] = 0;
+        p.ip_l3 = ip.l3;
         p.ip_job = true;
         jobs[2 * (size_t)i] = {m, ip.l3 + ip.hl, ip.l3, 0u};
       }
@@ -267,18 +378,18 @@ int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
       MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
       if (p.l4_job) {
         uint16_t c = res[2 * (size_t)i + 1];
-        if (p.udp && c == 0) c = 0xffff;  // ip_output.c:962-963
+        if (p.udp && c == 0) c = 0xffff;  // ip_output.c:962-963, ip6_output.c:193-194
         if (p.l4_store + 2 > m->m_len) {
           p.st |= UINET_TX_L4_LOST;  // ip_output.c:966-974: the reference gives up too
         } else {
           memcpy(m->m_data + p.l4_store, &c, 2);
           p.st |= UINET_TX_L4;
         }
-        pkthdr_of(m)->csum_flags &= ~(kCsumTcp | kCsumUdp);
+        pkthdr_of(m)->csum_flags &= ~p.clear;
       }
       if (p.ip_job) {
         const uint16_t c = res[2 * (size_t)i];
-        memcpy(m->m_data + p.ip.l3 + 10, &c, 2);
+        memcpy(m->m_data + p.ip_l3 + 10, &c, 2);
         p.st |= UINET_TX_IP;
         pkthdr_of(m)->csum_flags &= ~kCsumIp;
       }

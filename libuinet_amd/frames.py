@@ -14,6 +14,14 @@ each, or split into 2-3 mbufs after the headers.
 The mix covers what the hooks must tell apart: TCP, UDP, UDP without a
 checksum, IP options, 802.1Q tags, fragments, other protocols, non-IP
 frames, and (RX) corrupted headers / payloads / checksum fields.
+
+With ``ipv6 > 0`` that share of the IP frames is IPv6 instead (Ethernet type
+0x86dd): TCP / UDP directly after the fixed header with the in6_cksum_pseudo
+seed in the checksum field and CSUM_TCP_IPV6 / CSUM_UDP_IPV6 (tcp_output.c:
+1069-1071, udp6_usrreq.c:786), UDP with a zero checksum, fragments (next
+header 44), hop-by-hop options in front of TCP, ICMPv6, and global,
+link-local and (rarely) zone-carrying link-local addresses.  The IPv4 frames'
+random stream does not depend on ``ipv6``.
 """
 from __future__ import annotations
 
@@ -22,6 +30,7 @@ import numpy as np
 from .mbuf import MbufChains, aligned_empty
 
 CSUM_IP, CSUM_TCP, CSUM_UDP, CSUM_TSO = 0x1, 0x2, 0x4, 0x20
+CSUM_UDP_IPV6, CSUM_TCP_IPV6 = 0x2000, 0x4000
 
 
 def _in_pseudo(a: int, b: int, c: int) -> int:
@@ -35,17 +44,47 @@ def _bs16(x: int) -> int:
     return ((x & 0xFF) << 8) | ((x >> 8) & 0xFF)
 
 
+def pseudo6(src: bytes, dst: bytes, length: int, nxt: int) -> int:
+    """in6_cksum_pseudo(ip6, len, nxt, 0) for wire addresses (in6_cksum.c:
+    86-140): both addresses, htonl(len) and nxt as little-endian 16-bit
+    words, folded with end-around carry, not complemented."""
+    a = np.frombuffer(bytes(src) + bytes(dst), "<u2")
+    s = int(a.sum()) + _bs16(length >> 16) + _bs16(length & 0xFFFF) + _bs16(nxt)
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+def _addr6(rng) -> np.ndarray:
+    """Mostly global unicast; 15 % link-local (zone word 0 as on the wire);
+    3 % link-local with a nonzero zone word (ip6_input drops those)."""
+    a = rng.integers(0, 256, 16, dtype=np.uint8)
+    r = rng.random()
+    if r < 0.82:
+        a[0] = 0x20 | (a[0] & 0x0F)
+    else:
+        a[0:8] = (0xFE, 0x80, 0, 0, 0, 0, 0, 0)
+        if r > 0.97:
+            a[2:4] = (0, 1 + int(rng.integers(0, 255)))
+    return a
+
+
 class FrameBatch:
     """n frames (TX shape): ``tx`` chains + per-packet metadata."""
 
-    def __init__(self, n: int, seed: int = 1, vlan: float = 0.1, l2: bool = True):
+    def __init__(self, n: int, seed: int = 1, vlan: float = 0.1, l2: bool = True,
+                 ipv6: float = 0.0):
         rng = np.random.default_rng(seed)
+        rng6 = np.random.default_rng(seed + 0x6600)
         self.n = n
         self.l2 = l2
         kinds = rng.choice(["tcp", "udp", "udp0", "frag", "icmp", "arp"], n,
                            p=[0.6, 0.22, 0.04, 0.05, 0.05, 0.04] if l2 else
                            [0.62, 0.24, 0.04, 0.05, 0.05, 0.0])
         self.kinds = kinds
+        self.v6 = (rng6.random(n) < ipv6) & (kinds != "arp")
+        self.ext6 = self.v6 & (kinds == "tcp") & (rng6.random(n) < 0.06)
+        self.addr6 = np.zeros((n, 32), np.uint8)
         hdr_slot = 256
         pay = np.where(rng.random(n) < 0.15, rng.integers(0, 64, n), rng.integers(64, 1461, n))
         total_pay = int(pay.sum())
@@ -66,58 +105,16 @@ class FrameBatch:
         cursor = 0
         for i in range(n):
             k = kinds[i]
-            tag = l2 and rng.random() < vlan
-            l3 = (18 if tag else 14) if l2 else 0
-            hl = 20 if rng.random() < 0.85 else int(rng.integers(6, 16)) * 4
-            proto = {"tcp": 6, "udp": 17, "udp0": 17, "frag": 6, "icmp": 1, "arp": 0}[k]
-            l4h = 20 if proto == 6 else 8 if proto == 17 else 0
             p = int(pay[i])
-            ip_len = hl + l4h + p
-            h = np.zeros(l3 + hl + l4h, np.uint8)
-            if l2:
-                h[0:12] = rng.integers(0, 256, 12, dtype=np.uint8)
-                if tag:
-                    h[12:14] = (0x81, 0x00)
-                    h[14:16] = rng.integers(0, 256, 2, dtype=np.uint8)
-                h[l3 - 2:l3] = (0x08, 0x06) if k == "arp" else (0x08, 0x00)
-            ip = h[l3:l3 + hl]
-            ip[0] = 0x40 | (hl // 4)
-            ip[2:4] = (ip_len >> 8, ip_len & 0xFF)
-            ip[4:6] = rng.integers(0, 256, 2, dtype=np.uint8)
-            ip[6] = 0x20 if k == "frag" else 0x40
-            ip[8] = 64
-            ip[9] = proto
-            ip[12:16] = np.frombuffer(self.src[i].tobytes(), np.uint8)
-            ip[16:20] = np.frombuffer(self.dst[i].tobytes(), np.uint8)
-            if hl > 20:
-                ip[20:hl] = rng.integers(0, 256, hl - 20, dtype=np.uint8)
-            l4 = h[l3 + hl:]
-            l4[:] = rng.integers(0, 256, l4h, dtype=np.uint8)
-            fl = 0 if k == "arp" else CSUM_IP
-            if proto == 6:
-                l4[12] = 0x50
-                seed16 = _in_pseudo(int(self.src[i]), int(self.dst[i]), _bs16(l4h + 6 + p))
-                l4[16:18] = (seed16 & 0xFF, seed16 >> 8)  # native-order u16 store
-                if k != "frag":
-                    fl |= CSUM_TCP
-                    self.cdata[i] = 16
-            elif proto == 17:
-                ulen = 8 + p
-                l4[4:6] = (ulen >> 8, ulen & 0xFF)
-                if k == "udp0":
-                    l4[6:8] = 0
-                else:
-                    seed16 = _in_pseudo(int(self.src[i]), int(self.dst[i]), _bs16(ulen + 17))
-                    l4[6:8] = (seed16 & 0xFF, seed16 >> 8)
-                    fl |= CSUM_UDP
-                    self.cdata[i] = 6
-            if rng.random() < 0.02:
-                fl |= CSUM_TSO  # the hooks leave TSO packets to the driver
-            self.flags[i] = fl
+            if self.v6[i]:
+                h = self._header6(i, k, p, l2, vlan, rng6)
+            else:
+                h = self._header4(i, k, p, l2, vlan, rng)
+            if self.v6[i] and rng6.random() < 0.02:
+                self.flags[i] |= CSUM_TSO  # the hooks leave TSO packets to the driver
             ho = hdr_slot * i + 104  # m_pktdat (88) + max_linkhdr (16); <= 98 header bytes
             self.arena[ho:ho + h.size] = h
             self.hdr_off[i], self.hdr_len[i] = ho, h.size
-            self.l3[i], self.hlen[i] = l3, hl
             seg_off.append(ho)
             seg_len.append(h.size)
             # payload: the socket buffer's next p bytes, 1-2 page-cluster slices
@@ -134,6 +131,109 @@ class FrameBatch:
             pkt_seg.append(len(seg_off))
         self.tx = MbufChains(self.arena, seg_off, seg_len, pkt_seg)
         self.set_tx_flags()
+
+    def _header6(self, i, k, p, l2, vlan, rng):
+        """Link + IPv6 (+ one extension header) + L4 header of frame i."""
+        tag = l2 and rng.random() < vlan
+        l3 = (18 if tag else 14) if l2 else 0
+        ext = 8 if (k == "frag" or self.ext6[i]) else 0
+        nxt = {"tcp": 6, "frag": 6, "udp": 17, "udp0": 17, "icmp": 58}[k]
+        l4h = 20 if nxt == 6 else 8
+        plen = ext + l4h + p
+        h = np.zeros(l3 + 40 + ext + l4h, np.uint8)
+        if l2:
+            h[0:12] = rng.integers(0, 256, 12, dtype=np.uint8)
+            if tag:
+                h[12:14] = (0x81, 0x00)
+                h[14:16] = rng.integers(0, 256, 2, dtype=np.uint8)
+            h[l3 - 2:l3] = (0x86, 0xDD)
+        ip6 = h[l3:l3 + 40]
+        ip6[0] = 0x60
+        ip6[1:4] = rng.integers(0, 256, 3, dtype=np.uint8)
+        ip6[1] &= 0x0F
+        ip6[4:6] = (plen >> 8, plen & 0xFF)
+        ip6[6] = 44 if k == "frag" else 0 if ext else nxt
+        ip6[7] = 64
+        src, dst = _addr6(rng), _addr6(rng)
+        ip6[8:24], ip6[24:40] = src, dst
+        self.addr6[i] = np.concatenate([src, dst])
+        if ext:  # fragment header, or hop-by-hop with one PadN option
+            e = h[l3 + 40:l3 + 48]
+            e[0] = nxt
+            e[2:8] = rng.integers(0, 256, 6, dtype=np.uint8) if k == "frag" else (1, 4, 0, 0, 0, 0)
+        l4 = h[l3 + 40 + ext:]
+        l4[:] = rng.integers(0, 256, l4h, dtype=np.uint8)
+        fl, cd = 0, 0
+        if nxt == 6:
+            l4[12] = 0x50
+            seed16 = pseudo6(src, dst, l4h + p, 6)
+            l4[16:18] = (seed16 & 0xFF, seed16 >> 8)
+            if not ext:
+                fl, cd = CSUM_TCP_IPV6, 16
+        elif nxt == 17:
+            ulen = 8 + p
+            l4[4:6] = (ulen >> 8, ulen & 0xFF)
+            if k == "udp0":
+                l4[6:8] = 0
+            else:
+                seed16 = pseudo6(src, dst, ulen, 17)
+                l4[6:8] = (seed16 & 0xFF, seed16 >> 8)
+                fl, cd = CSUM_UDP_IPV6, 6
+        self.flags[i], self.cdata[i] = fl, cd
+        self.l3[i], self.hlen[i] = l3, 40 + ext
+        return h
+
+    def _header4(self, i, k, p, l2, vlan, rng):
+        """Link + IPv4 + L4 header of frame i (the original stream)."""
+        tag = l2 and rng.random() < vlan
+        l3 = (18 if tag else 14) if l2 else 0
+        hl = 20 if rng.random() < 0.85 else int(rng.integers(6, 16)) * 4
+        proto = {"tcp": 6, "udp": 17, "udp0": 17, "frag": 6, "icmp": 1, "arp": 0}[k]
+        l4h = 20 if proto == 6 else 8 if proto == 17 else 0
+        ip_len = hl + l4h + p
+        h = np.zeros(l3 + hl + l4h, np.uint8)
+        if l2:
+            h[0:12] = rng.integers(0, 256, 12, dtype=np.uint8)
+            if tag:
+                h[12:14] = (0x81, 0x00)
+                h[14:16] = rng.integers(0, 256, 2, dtype=np.uint8)
+            h[l3 - 2:l3] = (0x08, 0x06) if k == "arp" else (0x08, 0x00)
+        ip = h[l3:l3 + hl]
+        ip[0] = 0x40 | (hl // 4)
+        ip[2:4] = (ip_len >> 8, ip_len & 0xFF)
+        ip[4:6] = rng.integers(0, 256, 2, dtype=np.uint8)
+        ip[6] = 0x20 if k == "frag" else 0x40
+        ip[8] = 64
+        ip[9] = proto
+        ip[12:16] = np.frombuffer(self.src[i].tobytes(), np.uint8)
+        ip[16:20] = np.frombuffer(self.dst[i].tobytes(), np.uint8)
+        if hl > 20:
+            ip[20:hl] = rng.integers(0, 256, hl - 20, dtype=np.uint8)
+        l4 = h[l3 + hl:]
+        l4[:] = rng.integers(0, 256, l4h, dtype=np.uint8)
+        fl = 0 if k == "arp" else CSUM_IP
+        if proto == 6:
+            l4[12] = 0x50
+            seed16 = _in_pseudo(int(self.src[i]), int(self.dst[i]), _bs16(l4h + 6 + p))
+            l4[16:18] = (seed16 & 0xFF, seed16 >> 8)  # native-order u16 store
+            if k != "frag":
+                fl |= CSUM_TCP
+                self.cdata[i] = 16
+        elif proto == 17:
+            ulen = 8 + p
+            l4[4:6] = (ulen >> 8, ulen & 0xFF)
+            if k == "udp0":
+                l4[6:8] = 0
+            else:
+                seed16 = _in_pseudo(int(self.src[i]), int(self.dst[i]), _bs16(ulen + 17))
+                l4[6:8] = (seed16 & 0xFF, seed16 >> 8)
+                fl |= CSUM_UDP
+                self.cdata[i] = 6
+        if rng.random() < 0.02:
+            fl |= CSUM_TSO  # the hooks leave TSO packets to the driver
+        self.flags[i] = fl
+        self.l3[i], self.hlen[i] = l3, hl
+        return h
 
     def set_tx_flags(self) -> None:
         first = self.tx.pkt_seg[:-1]

@@ -18,6 +18,17 @@
  *   TX  sys/netinet/ip_output.c:953-976   in_delayed_cksum
  *       sys/netinet/ip_output.c:665-667   ip_sum = 0; ip_sum = in_cksum(m, hlen)
  *
+ * IPv6 frames (Ethernet type 0x86dd, or version 6 at l2len) go the IPv6 way:
+ *   RX  sys/netinet6/ip6_input.c          short chains and embedded zones
+ *                                         (:658-661) are dropped; the next
+ *                                         header picks the transport
+ *       sys/netinet/tcp_input.c:627-639   th_sum = in6_cksum(m, TCP, 40, tlen)
+ *       sys/netinet6/udp6_usrreq.c:216-246 uh_ulen == payload length, uh_sum
+ *                                         != 0, in6_cksum(m, UDP, 40, ulen)
+ *     with the same CSUM_DATA_VALID(_IPV6) | CSUM_PSEUDO_HDR marks;
+ *   TX  sys/netinet6/ip6_output.c:188-209,966-981  in6_delayed_cksum(m,
+ *                                         ip6_plen, sizeof(struct ip6_hdr))
+ *
  * Chains whose link header reaches past the first mbuf are viewed through
  * a private copy of their mbuf headers (what m_adj would leave).
  */
@@ -36,6 +47,8 @@
 #define O_CSUM_IP_VALID 0x200
 #define O_CSUM_DATA_VALID 0x400
 #define O_CSUM_PSEUDO_HDR 0x800
+#define O_CSUM_UDP_IPV6 0x2000
+#define O_CSUM_TCP_IPV6 0x4000
 
 /* status bits, as include/uinet_cksum.h defines them */
 #define S_RX_IPV4 0x01
@@ -44,10 +57,12 @@
 #define S_RX_L4_OK 0x08
 #define S_RX_NOSUM 0x10
 #define S_RX_FRAG 0x20
+#define S_RX_IPV6 0x40
 #define S_TX_L4 0x01
 #define S_TX_IP 0x02
 #define S_TX_L4_LOST 0x04
 #define S_TX_SKIP 0x08
+#define S_TX_IPV6 0x10
 
 /* struct pkthdr's checksum fields (sys/sys/mbuf.h:116-133) */
 static int *
@@ -119,15 +134,21 @@ chain_total(const struct oracle_mbuf *m)
 	return t;
 }
 
-/* Offset of the IPv4 header (l2len -1: Ethernet, optional 802.1Q), or -1. */
+/* Offset of the network header (l2len -1: Ethernet, optional 802.1Q), or -1;
+ * *ver = 4 or 6 (ether_demux's type switch, or the version nibble at l2len). */
 static int
-ip_offset(const struct oracle_mbuf *m, int l2len)
+ip_offset(const struct oracle_mbuf *m, int l2len, int *ver)
 {
 	uint8_t e[18];
-	int got, type;
+	int got, type, l3 = 14;
 
-	if (l2len >= 0)
-		return l2len;
+	*ver = 0;
+	if (l2len >= 0) {
+		if (chain_bytes(m, l2len, e, 1) < 1)
+			return -1;
+		*ver = e[0] >> 4;
+		return (*ver == 4 || *ver == 6) ? l2len : -1;
+	}
 	got = chain_bytes(m, 0, e, 18);
 	if (got < 14)
 		return -1;
@@ -136,11 +157,51 @@ ip_offset(const struct oracle_mbuf *m, int l2len)
 		if (got < 18)
 			return -1;
 		type = e[16] << 8 | e[17];
-		if (type == 0x0800)
-			return 18;
-		return -1;
+		l3 = 18;
 	}
-	return type == 0x0800 ? 14 : -1;
+	*ver = type == 0x0800 ? 4 : type == 0x86dd ? 6 : 0;
+	return *ver ? l3 : -1;
+}
+
+/* in6_clearscope's test (ip6_input.c:658): a link-local unicast or link- /
+ * interface-local multicast address with a nonzero zone word. */
+static int
+zone_embedded(const uint8_t *a)
+{
+	int ll = a[0] == 0xfe && (a[1] & 0xc0) == 0x80;
+	int mc = a[0] == 0xff && ((a[1] & 0x0f) == 0x02 || (a[1] & 0x0f) == 0x01);
+
+	return (ll || mc) && (a[2] || a[3]);
+}
+
+/* One received IPv6 frame, m_data at the IPv6 header in `ipm`. */
+static uint8_t
+rx6(struct oracle_mbuf *m, struct oracle_mbuf *ipm, const uint8_t *h, int got, long avail)
+{
+	uint8_t st = S_RX_IPV6;
+	int plen = h[4] << 8 | h[5], nxt = h[6], sum;
+
+	if (nxt == 44)
+		st |= S_RX_FRAG;	/* frag6_input reassembles first */
+	if (plen == 0 || avail < 40 + (long)plen)
+		return st;		/* jumbogram (hop-by-hop), ip6s_tooshort */
+	if (zone_embedded(h + 8) || zone_embedded(h + 24))
+		return st;		/* ip6s_badscope */
+	if (nxt == 17) {
+		if (got < 48 || (h[44] << 8 | h[45]) != plen)
+			return st;	/* udps_badlen */
+		if ((h[46] | h[47]) == 0)
+			return st | S_RX_NOSUM;
+	} else if (nxt != 6) {
+		return st;
+	}
+	sum = oracle_in6_cksum(ipm, (uint8_t)nxt, 40, (uint32_t)plen);
+	st |= S_RX_L4 | (sum == 0 ? S_RX_L4_OK : 0);
+	if (m->m_flags & O_M_PKTHDR) {
+		*csum_flags(m) |= O_CSUM_DATA_VALID | O_CSUM_PSEUDO_HDR;
+		*csum_data(m) = sum ^ 0xffff;
+	}
+	return st;
 }
 
 void
@@ -153,10 +214,18 @@ oracle_rx_offload(struct oracle_mbuf *const *mv, int n, int l2len, uint8_t *stat
 		uint8_t h[60 + 8], st = 0;
 		int l3, got, hlen, ip_len, frag, proto, sum;
 		uint32_t src, dst;
+		int ver;
 
-		if (!m || (l3 = ip_offset(m, l2len)) < 0)
+		if (!m || (l3 = ip_offset(m, l2len, &ver)) < 0)
 			goto done;
 		got = chain_bytes(m, l3, h, (int)sizeof(h));
+		if (ver == 6) {
+			if (got < 40 || (h[0] >> 4) != 6)
+				goto done;
+			ipm = adj_view(m, l3, &tmp);
+			st = rx6(m, ipm, h, got, chain_total(m) - l3);
+			goto done;
+		}
 		if (got < 20 || (h[0] >> 4) != 4)
 			goto done;
 		hlen = (h[0] & 15) << 2;
@@ -219,16 +288,42 @@ oracle_tx_offload(struct oracle_mbuf *const *mv, int n, int l2len, uint8_t *stat
 
 	for (i = 0; i < n; i++) {
 		struct oracle_mbuf *m = mv[i], *tmp = NULL, *ipm;
-		uint8_t h[20], st = 0;
-		int l3, hlen, ip_len, fl;
+		uint8_t h[40], st = 0;
+		int l3, hlen, ip_len, fl, ver = 0;
 
 		if (!m || !(m->m_flags & O_M_PKTHDR)) {
 			st = S_TX_SKIP;
 			goto done;
 		}
 		fl = *csum_flags(m);
+		if (!(fl & O_CSUM_TSO) && (l3 = ip_offset(m, l2len, &ver)) >= 0 && ver == 6) {
+			/* in6_delayed_cksum(m, plen, sizeof(struct ip6_hdr)) */
+			uint16_t csum;
+			int plen, offset;
+
+			if (!(fl & (O_CSUM_TCP_IPV6 | O_CSUM_UDP_IPV6)) ||
+			    chain_bytes(m, l3, h, 40) < 40 || (h[0] >> 4) != 6 ||
+			    (plen = h[4] << 8 | h[5]) == 0) {
+				st = S_TX_SKIP;
+				goto done;
+			}
+			ipm = adj_view(m, l3, &tmp);
+			csum = oracle_cksum_skip(ipm, 40 + plen, 40);
+			if ((fl & O_CSUM_UDP_IPV6) && csum == 0)
+				csum = 0xffff;
+			offset = 40 + *csum_data(m);
+			st = S_TX_IPV6;
+			if (offset + 2 > ipm->m_len) {
+				st |= S_TX_L4_LOST;
+			} else {
+				memcpy(ipm->m_data + offset, &csum, 2);
+				st |= S_TX_L4;
+			}
+			*csum_flags(m) &= ~(O_CSUM_TCP_IPV6 | O_CSUM_UDP_IPV6);
+			goto done;
+		}
 		if ((fl & O_CSUM_TSO) || !(fl & (O_CSUM_IP | O_CSUM_TCP | O_CSUM_UDP)) ||
-		    (l3 = ip_offset(m, l2len)) < 0 || chain_bytes(m, l3, h, 20) < 20 ||
+		    ver != 4 || chain_bytes(m, l3, h, 20) < 20 ||
 		    (h[0] >> 4) != 4 || (hlen = (h[0] & 15) << 2) < 20) {
 			st = S_TX_SKIP;
 			goto done;

@@ -16,7 +16,8 @@ import pytest
 from libuinet_amd.frames import FrameBatch, pkthdr_fields
 
 RX_IPV4, RX_IP_OK, RX_L4, RX_L4_OK, RX_NOSUM, RX_FRAG = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
-TX_L4, TX_IP, TX_L4_LOST, TX_SKIP = 0x01, 0x02, 0x04, 0x08
+RX_IPV6 = 0x40
+TX_L4, TX_IP, TX_L4_LOST, TX_SKIP, TX_IPV6 = 0x01, 0x02, 0x04, 0x08, 0x10
 CSUM_IP_CHECKED, CSUM_IP_VALID, CSUM_DATA_VALID, CSUM_PSEUDO_HDR = 0x100, 0x200, 0x400, 0x800
 
 
@@ -43,7 +44,7 @@ def _ip_len(b, l3):
 
 @pytest.fixture(scope="module")
 def frames():
-    return lambda seed=11, n=2500, l2=True: FrameBatch(n, seed=seed, l2=l2)
+    return lambda seed=11, n=2500, l2=True, ipv6=0.0: FrameBatch(n, seed=seed, l2=l2, ipv6=ipv6)
 
 
 def test_tx_oracle_against_reference(frames, ora, ref):
@@ -111,9 +112,95 @@ def test_rx_oracle_against_reference(frames, ora, ref):
         assert bool(st[i] & RX_L4_OK) == (want == 0)
     # uncorrupted TCP/UDP frames all verify; a corrupted one never both verifies
     good = ~bad & np.isin(fb.kinds, ["tcp", "udp"]) & ((fb.flags & 0x20) == 0)
-    assert (st[good] & (RX_IP_OK | RX_L4_OK) == (RX_IP_OK | RX_L4_OK)).all()
+    assert ((st[good] & (RX_IP_OK | RX_L4_OK)) == (RX_IP_OK | RX_L4_OK)).all()
     assert ((st[np.isin(fb.kinds, ["udp0"])] & RX_NOSUM) != 0).all()
     assert ((st[fb.kinds == "frag"] & RX_FRAG) != 0).all()
+
+
+# ---- IPv6 (ip6_output.c:188-209,966-981; tcp_input.c:627-639; udp6_usrreq.c:216-246)
+
+def _zoned(a: np.ndarray) -> bool:
+    """A link-local / link- or interface-local multicast address with a zone
+    word (ip6_input.c:658-661 drops the packet)."""
+    ll = a[0] == 0xFE and (a[1] & 0xC0) == 0x80
+    mc = a[0] == 0xFF and (a[1] & 0x0F) in (1, 2)
+    return bool((ll or mc) and (a[2] or a[3]))
+
+
+def _from_l3(ch, fb, idx):
+    """Packets ``idx`` of chains ``ch`` copied from their network header on,
+    one mbuf each (the view in6_cksum reads: m_data at the IPv6 header)."""
+    from libuinet_amd.mbuf import MbufChains, aligned_empty
+
+    bufs = [ch.packet_bytes(int(i))[int(fb.l3[i]):] for i in idx]
+    arena = aligned_empty(2048 * max(1, len(bufs)) + 64)
+    for j, b in enumerate(bufs):
+        arena[2048 * j:2048 * j + len(b)] = np.frombuffer(b, np.uint8)
+    return MbufChains.contiguous(arena, 2048 * np.arange(len(bufs)), [len(b) for b in bufs]), bufs
+
+
+def test_tx6_oracle_against_reference(frames, ora, ref):
+    """IPv6 TX: the frames' checksum-field seeds are the reference's own
+    in6_cksum_pseudo; after the oracle TX hook every handled IPv6 packet
+    verifies to 0 with the reference's in6_cksum, and the handled
+    CSUM_*_IPV6 bits are cleared."""
+    fb = frames(seed=13, ipv6=0.5)
+    v6 = np.flatnonzero(fb.v6 & ((fb.flags & 0x6000) != 0))
+    assert v6.size > 500
+    for i in v6[:300]:  # the builder's seed == the reference's in6_cksum_pseudo(ip6, len, nxt, 0)
+        b = np.frombuffer(fb.frame_bytes(i), np.uint8)
+        l3 = int(fb.l3[i])
+        ip6 = b[l3:l3 + 40].copy()
+        nxt, plen = int(ip6[6]), int(ip6[4]) << 8 | int(ip6[5])
+        off = l3 + 40 + (16 if nxt == 6 else 6)
+        stored = int(b[off]) | int(b[off + 1]) << 8
+        if not (_zoned(fb.addr6[i][:16]) or _zoned(fb.addr6[i][16:])):
+            assert ref.in6_cksum_pseudo(ip6.ctypes.data, plen, nxt, 0) == stored
+    st = ora.tx_offload(fb.tx.heads)
+    tso = (fb.flags & 0x20) != 0
+    want = fb.v6 & ((fb.flags & 0x6000) != 0) & ~tso
+    assert (((st & TX_IPV6) != 0) == want).all()
+    assert ((st[want] & (TX_L4 | TX_L4_LOST)) == TX_L4).all()
+    fl, _ = pkthdr_fields(fb.tx)
+    assert not (fl[want] & 0x6000).any()
+    assert ((st[fb.v6 & ~want] & TX_SKIP) != 0).all()
+    ok = np.array([i for i in np.flatnonzero(want)
+                   if not (_zoned(fb.addr6[i][:16]) or _zoned(fb.addr6[i][16:]))])
+    ch, bufs = _from_l3(fb.tx, fb, ok)
+    nxt = np.array([b[6] for b in bufs])
+    plen = np.array([b[4] << 8 | b[5] for b in bufs])
+    assert not ref.in6_cksum_batch(ch.heads, nxt, 40, plen).any()
+
+
+def test_rx6_oracle_against_reference(frames, ora, ref):
+    """IPv6 RX: every L4 mark the oracle hook writes encodes the reference's
+    own in6_cksum over the received bytes, corrupted frames included; the
+    frames the stack would not checksum through tcp6/udp6 get none."""
+    fb = frames(seed=14, ipv6=0.5)
+    ora.tx_offload(fb.tx.heads)
+    rx, arena, bad = fb.rx(seed=7, corrupt=0.2)
+    st = ora.rx_offload(rx.heads)
+    fl, cd = pkthdr_fields(rx)
+    assert (((st & RX_IPV6) != 0) == fb.v6).all()
+    assert not (st[fb.v6] & (RX_IPV4 | RX_IP_OK)).any()
+    l4 = np.flatnonzero(fb.v6 & ((st & RX_L4) != 0))
+    assert l4.size > 500
+    ch, bufs = _from_l3(rx, fb, l4)
+    nxt = np.array([b[6] for b in bufs])
+    plen = np.array([b[4] << 8 | b[5] for b in bufs])
+    assert set(np.unique(nxt)) <= {6, 17}
+    want = ref.in6_cksum_batch(ch.heads, nxt, 40, plen)
+    np.testing.assert_array_equal(cd[l4] ^ 0xFFFF, want)
+    np.testing.assert_array_equal((st[l4] & RX_L4_OK) != 0, want == 0)
+    assert ((fl[l4] & 0xC00) == 0xC00).all()
+    zoned = np.array([_zoned(a[:16]) or _zoned(a[16:]) for a in fb.addr6])
+    clean = fb.v6 & ~bad & ~zoned & ~fb.ext6
+    good = clean & np.isin(fb.kinds, ["tcp", "udp"]) & ((fb.flags & 0x20) == 0)  # TSO: not filled
+    assert ((st[good] & (RX_L4 | RX_L4_OK)) == (RX_L4 | RX_L4_OK)).all()
+    assert not (st[fb.v6 & zoned] & RX_L4).any()
+    assert not (st[fb.v6 & fb.ext6] & RX_L4).any()
+    assert ((st[clean & (fb.kinds == "udp0")] & RX_NOSUM) != 0).all()
+    assert ((st[clean & (fb.kinds == "frag")] & RX_FRAG) != 0).all()
 
 
 # ---- GPU: engine == oracle ------------------------------------------------------
@@ -155,6 +242,46 @@ def test_offload_gpu_matches_oracle(torch_dev, frames, ora, l2, zero_copy):
     for x, y in zip(pkthdr_fields(rx_a), pkthdr_fields(rx_b)):
         np.testing.assert_array_equal(x, y)
     assert ((st_g & RX_L4_OK) != 0).any() and (((st_g & RX_L4) != 0) & ((st_g & RX_L4_OK) == 0)).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("l2,zero_copy", [(True, False), (True, True), (False, False)])
+def test_offload6_gpu_matches_oracle(torch_dev, frames, ora, l2, zero_copy):
+    """A mixed IPv4 / IPv6 batch through both hooks: the engine's bytes,
+    marks and status equal the oracle's."""
+    import libuinet_amd as u
+
+    l2len = -1 if l2 else 0
+    a, b = frames(seed=23, l2=l2, ipv6=0.4), frames(seed=23, l2=l2, ipv6=0.4)
+    if zero_copy:
+        u.register_host(a.arena)
+    try:
+        st_g = u.tx_offload(a.tx.heads, l2len)
+    finally:
+        if zero_copy:
+            u.unregister_host(a.arena)
+    st_o = ora.tx_offload(b.tx.heads, l2len)
+    np.testing.assert_array_equal(st_g, st_o)
+    np.testing.assert_array_equal(a.arena, b.arena)
+    for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
+        np.testing.assert_array_equal(x, y)
+    assert ((st_g & (TX_IPV6 | TX_L4)) == (TX_IPV6 | TX_L4)).sum() > 300
+    rx_a, arena_a, _ = a.rx(seed=8, corrupt=0.15)
+    rx_b, arena_b, _ = b.rx(seed=8, corrupt=0.15)
+    if zero_copy:
+        u.register_host(arena_a)
+    try:
+        st_g = u.rx_offload(rx_a.heads, l2len)
+    finally:
+        if zero_copy:
+            u.unregister_host(arena_a)
+    st_o = ora.rx_offload(rx_b.heads, l2len)
+    np.testing.assert_array_equal(st_g, st_o)
+    for x, y in zip(pkthdr_fields(rx_a), pkthdr_fields(rx_b)):
+        np.testing.assert_array_equal(x, y)
+    v6 = (st_g & RX_IPV6) != 0
+    assert (v6 & ((st_g & RX_L4_OK) != 0)).sum() > 300
+    assert (v6 & ((st_g & RX_L4) != 0) & ((st_g & RX_L4_OK) == 0)).any()
 
 
 @pytest.mark.gpu
