@@ -118,10 +118,13 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 // Build-time occupancy override for A/B (-DUINET_CHAINS_WAVES=7|8 forces that
 // many waves per SIMD, spilling what does not fit); unset = the compiler's 80
 // VGPRs, occupancy 6.
+// The default holds the kPass = 2 kernel at 6 waves per SIMD (80 VGPRs, no
+// spills): left alone the compiler takes 88 for the interleaved consume and
+// drops to 5.
 #ifdef UINET_CHAINS_WAVES
 #define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(UINET_CHAINS_WAVES)))
 #else
-#define UINET_CHAINS_OCC
+#define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(kPass == 2 ? 6 : 1)))
 #endif
 
 template <int kPass, int kTile, typename OffT, typename LenT>
@@ -159,16 +162,24 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
   u32x4 va[kPass], vb[kPass];
   uint32_t ka[kPass], kb[kPass];
   uint32_t pend = 0;
+  // The passes' chunk sums first, then their prefix sums side by side (the
+  // DPP chains interleave: +1.3-3 % on config 3, profiles/r02/ab_lab/), then
+  // the bin updates.
   auto consume = [&](const u32x4 (&v)[kPass], const uint32_t (&key)[kPass]) {
+    uint32_t P[kPass], sl[kPass], nx[kPass];
+#pragma unroll
+    for (int q = 0; q < kPass; ++q) P[q] = lut.sum_oc_idx(v[q], key[q] & 0xffffu);  // < 2^17
 #pragma unroll
     for (int q = 0; q < kPass; ++q) {
-      const uint32_t w = lut.sum_oc_idx(v[q], key[q] & 0xffffu);  // < 2^17
-      const uint32_t sl = key[q] >> 16;
-      const uint32_t P = wave_scan<0, false>(w, 0u);  // < 2^23
-      const uint32_t nx = wave_shl1(sl);
-      if (lane == 63 || nx != sl) {
-        atomicAdd(&acc[sl], (unsigned long long)P);
-        if (lane != 63) atomicAdd(&acc[nx], (unsigned long long)(-(long long)P));
+      sl[q] = key[q] >> 16;
+      nx[q] = wave_shl1(sl[q]);
+    }
+    wave_scan_add_n<kPass>(P);  // < 2^23
+#pragma unroll
+    for (int q = 0; q < kPass; ++q) {
+      if (lane == 63 || nx[q] != sl[q]) {
+        atomicAdd(&acc[sl[q]], (unsigned long long)P[q]);
+        if (lane != 63) atomicAdd(&acc[nx[q]], (unsigned long long)(-(long long)P[q]));
       }
     }
   };

@@ -252,6 +252,23 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t key) {
   return x;
 }
 
+// kN independent inclusive add-scans over the wave, issued step by step side
+// by side so each chain's DPP read-after-write wait fills with the others'
+// steps instead of s_nops.  All 64 lanes must be active.
+template <int kN>
+__device__ __forceinline__ void wave_scan_add_n(uint32_t (&x)[kN]) {
+#define UINET_DPP_STEP_N(CTRL, RMASK)                                                     \
+  _Pragma("unroll") for (int i = 0; i < kN; ++i) x[i] +=                                 \
+      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[i], CTRL, RMASK, 0xf, true);
+  UINET_DPP_STEP_N(0x111, 0xf)  // row_shr:1
+  UINET_DPP_STEP_N(0x112, 0xf)  // row_shr:2
+  UINET_DPP_STEP_N(0x114, 0xf)  // row_shr:4
+  UINET_DPP_STEP_N(0x118, 0xf)  // row_shr:8
+  UINET_DPP_STEP_N(0x142, 0xa)  // row_bcast:15 -> rows 1, 3
+  UINET_DPP_STEP_N(0x143, 0xc)  // row_bcast:31 -> rows 2, 3
+#undef UINET_DPP_STEP_N
+}
+
 // The hardware deals blocks round-robin over the 8 XCDs (block b on XCD
 // b % 8), each with its own L2.  With `remap`, block b takes logical id
 // (b % 8) * (grid / 8) + b / 8, so an XCD's blocks work on one contiguous band

@@ -40,6 +40,22 @@ int check_launch() { return record_hip(hipGetLastError()); }
 
 namespace lab {
 
+// kN independent inclusive add-scans over the wave, step by step side by side
+// so the DPP read-after-write waits of one chain fill with the others' work.
+template <int kN>
+__device__ __forceinline__ void wave_scan_n(uint32_t (&x)[kN]) {
+#define LAB_STEP(CTRL, RMASK)                                                                 \
+  _Pragma("unroll") for (int i = 0; i < kN; ++i) x[i] +=                                     \
+      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[i], CTRL, RMASK, 0xf, true);
+  LAB_STEP(0x111, 0xf)
+  LAB_STEP(0x112, 0xf)
+  LAB_STEP(0x114, 0xf)
+  LAB_STEP(0x118, 0xf)
+  LAB_STEP(0x142, 0xa)
+  LAB_STEP(0x143, 0xc)
+#undef LAB_STEP
+}
+
 // ---------------------------------------------------------------------------
 // k_lps: one lane per segment.  The descriptor round is k_chains_pipe's; then
 // each lane streams its own segment's chunks, kU per step, double-buffered,
@@ -370,7 +386,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
                                                        const uint32_t* __restrict__ seed,
                                                        uint16_t* __restrict__ out, uint32_t n,
                                                        uint32_t flags, uint32_t long_ch) {
-  static_assert(kTile >= 1 && kTile <= 32,
+  static_assert(kTile >= 1 && kTile <= 63,
                 "a tile's packets are one per lane, lane kTile reads the end of its segment "
                 "range, and its 2 * kTile bins are one per lane");
   constexpr int kWin = 64 * kPass;  // chunks per batch of passes
@@ -396,9 +412,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
   uint32_t ka[kPass], kb[kPass];
   uint32_t pend = 0;
   uint32_t dummy = 0;
-  auto consume = [&](const u32x4 (&v)[kPass], const uint32_t (&key)[kPass]) {
+  auto consume = [&](const auto& v, const auto& key) {
+    constexpr int NP = sizeof(key) / sizeof(key[0]);
+    if constexpr (kAbl == 8 || kAbl == 11) {
+      // every pass's chunk sums first, then the passes' scans side by side
+      // (independent DPP chains interleave), then the bin updates
+      uint32_t P[NP], sl[NP], nx[NP];
 #pragma unroll
-    for (int q = 0; q < kPass; ++q) {
+      for (int q = 0; q < NP; ++q) P[q] = lut.sum_oc_idx(v[q], key[q] & 0xffffu);
+#pragma unroll
+      for (int q = 0; q < NP; ++q) { sl[q] = key[q] >> 16; nx[q] = wave_shl1(sl[q]); }
+      wave_scan_n<NP>(P);
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        if (lane == 63 || nx[q] != sl[q]) {
+          atomicAdd(&acc[sl[q]], (unsigned long long)P[q]);
+          if (lane != 63) atomicAdd(&acc[nx[q]], (unsigned long long)(-(long long)P[q]));
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
       if constexpr (kAbl == 1) { dummy ^= v[q].x ^ v[q].y ^ v[q].z ^ v[q].w ^ key[q]; continue; }
       const uint32_t w = lut.sum_oc_idx(v[q], key[q] & 0xffffu);  // < 2^17
       if constexpr (kAbl == 3) { dummy += w; continue; }
@@ -423,6 +458,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
     const uint32_t S0 = __builtin_amdgcn_readfirstlane(ps);
     const uint32_t S1 = __builtin_amdgcn_readlane(ps, np);
     if (lane < 2 * kTile) acc[lane] = 0;
+    if (kTile > 32 && lane + 64 < 2 * kTile) acc[lane + 64] = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     uint32_t carry_slot1 = 0;  // slot + 1 of the last segment of the previous round
     uint32_t carry_pos = 0;    // chain offset just past that segment
@@ -505,6 +541,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
         if (lane == 0) atomicAdd(&acc[mts], (unsigned long long)x);
       }
       // --- the round's chunk list -----------------------------------------
+      if constexpr (kAbl == 9) { dummy += nch ^ (uint32_t)c0; continue; }
       const uint32_t nch_l = is_long ? 0u : nch;
       const uint32_t ci = wave_scan<0, false>(nch_l, 0u);
       const uint32_t cst = ci - nch_l;
@@ -525,23 +562,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
       uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the batch
       // Issue the batch at list chunk b into (v, key): segment lookup, mask
       // index and bin, loads.  Nothing here waits for packet bytes.
-      auto issue = [&](uint32_t b, u32x4 (&v)[kPass], uint32_t (&key)[kPass], auto kWindow) {
-        const bool mk = nch_l != 0 && cst >= b && cst < b + kWin;
+      auto issue = [&](uint32_t b, auto& v, auto& key, auto kWindow) {
+        constexpr int NP = sizeof(key) / sizeof(key[0]);
+        const bool mk = nch_l != 0 && cst >= b && cst < b + 64u * NP;
         if (mk) mark[cst - b] = (uint8_t)(lane + 1);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        uint32_t sc1[kPass];
+        uint32_t sc1[NP];
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) sc1[q] = mark[q * 64 + lane];
+        for (int q = 0; q < NP; ++q) sc1[q] = mark[q * 64 + lane];
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) sc1[q] = wave_scan<1, false>(sc1[q], 0u);
+        for (int q = 0; q < NP; ++q) sc1[q] = wave_scan<1, false>(sc1[q], 0u);
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) {
+        for (int q = 0; q < NP; ++q) {
           const uint32_t last = __builtin_amdgcn_readlane(sc1[q], 63);
           sc1[q] = max(sc1[q], carry_seg1);
           carry_seg1 = max(carry_seg1, last);
         }
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) {
+        for (int q = 0; q < NP; ++q) {
           const uint32_t c = b + (uint32_t)(q * 64 + lane);
           const bool in = c < C;
           const uint32_t cc = in ? c : C - 1;  // past the end: the last chunk, masked
@@ -584,6 +622,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
             if (!more2) break;
             b += kWin;
           }
+        } else if constexpr (kAbl == 10 || kAbl == 11) {
+          // full batches of kPass passes, then an odd last pass on its own
+          // (issued before the last full batch is consumed): no empty pass
+          const uint32_t npass = (C + 63u) / 64u;
+          const uint32_t Cfull = (npass / kPass) * kWin;
+          for (uint32_t b = 0; b < Cfull; b += kWin) {
+            issue(b, vb, kb, kWindow);
+            if (pend) consume(va, ka);
+#pragma unroll
+            for (int q = 0; q < kPass; ++q) {
+              va[q] = vb[q];
+              ka[q] = kb[q];
+            }
+            pend = 1;
+          }
+          if (Cfull < C) {
+            u32x4 v1[1];
+            uint32_t k1[1];
+            issue(Cfull, v1, k1, kWindow);
+            if (pend) consume(va, ka);
+            consume(v1, k1);
+          } else if (pend) {
+            consume(va, ka);
+          }
+          pend = 0;
         } else {
         for (uint32_t b = 0; b < C; b += kWin) {
           issue(b, vb, kb, kWindow);
@@ -608,7 +671,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
     if (lane < np) {
       const uint32_t p = P0 + (uint32_t)lane;
       const uint32_t odd = fold16(acc[2 * lane + 1]);
-      out[p] = finish(acc[2 * lane] + rot8(odd) + (seed ? seed[p] : 0u) + (kAbl && kAbl != 4 ? dummy : 0u), flags);
+      out[p] = finish(acc[2 * lane] + rot8(odd) + (seed ? seed[p] : 0u) + (kAbl && kAbl != 4 && kAbl < 8 ? dummy : 0u), flags);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
@@ -654,6 +717,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
   uint32_t pend = 0;
   uint32_t dummy = 0;
   auto consume = [&](const u32x4 (&v)[kPass], const uint32_t (&key)[kPass]) {
+    if constexpr (kAbl == 8) {
+      // every pass's chunk sums first, then the passes' scans side by side
+      // (independent DPP chains interleave), then the bin updates
+      uint32_t P[kPass], sl[kPass], nx[kPass];
+#pragma unroll
+      for (int q = 0; q < kPass; ++q) P[q] = lut.sum_oc_idx(v[q], key[q] & 0xffffu);
+#pragma unroll
+      for (int q = 0; q < kPass; ++q) { sl[q] = key[q] >> 16; nx[q] = wave_shl1(sl[q]); }
+      wave_scan_n<kPass>(P);
+#pragma unroll
+      for (int q = 0; q < kPass; ++q) {
+        if (lane == 63 || nx[q] != sl[q]) {
+          atomicAdd(&acc[sl[q]], (unsigned long long)P[q]);
+          if (lane != 63) atomicAdd(&acc[nx[q]], (unsigned long long)(-(long long)P[q]));
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < kPass; ++q) {
       if constexpr (kAbl == 1) { dummy ^= v[q].x ^ v[q].y ^ v[q].z ^ v[q].w ^ key[q]; continue; }
@@ -789,6 +870,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
         if (lane == 0) atomicAdd(&acc[mts], (unsigned long long)x);
       }
       // --- the round's chunk list -----------------------------------------
+      if constexpr (kAbl == 9) { dummy += nch ^ (uint32_t)c0; continue; }
       const uint32_t nch_l = is_long ? 0u : nch;
       const uint32_t ci = wave_scan<0, false>(nch_l, 0u);
       const uint32_t cst = ci - nch_l;
@@ -898,7 +980,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
     if (lane < np) {
       const uint32_t p = P0 + (uint32_t)lane;
       const uint32_t odd = fold16(acc[2 * lane + 1]);
-      out[p] = finish(acc[2 * lane] + rot8(odd) + (seed ? seed[p] : 0u) + (kAbl && kAbl != 4 ? dummy : 0u), flags);
+      out[p] = finish(acc[2 * lane] + rot8(odd) + (seed ? seed[p] : 0u) + (kAbl && kAbl != 4 && kAbl < 8 ? dummy : 0u), flags);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
@@ -1016,6 +1098,17 @@ int main(int argc, char** argv) {
   ADD("pingpong P2", true, hipLaunchKernelGGL((lab::k_pipe_abl<4, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   ADD("pingpong P1", true, hipLaunchKernelGGL((lab::k_pipe_abl<4, 1, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   ADD("pingpong P3", true, hipLaunchKernelGGL((lab::k_pipe_abl<4, 3, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
+  // lab7: descriptor rounds only (no chunk list, no loads of packet bytes)
+  ADD("abl9 descriptor rounds only", false, hipLaunchKernelGGL((lab::k_pipe_abl<9, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
+  // lab9: tiles of 63 / 16 packets (fewer / more partial descriptor rounds)
+  ADD("tile63 consume interleaved", true, hipLaunchKernelGGL((lab::k_pipe_abl<8, 2, 63, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 63)), KARGS))
+  ADD("tile48 consume interleaved", true, hipLaunchKernelGGL((lab::k_pipe_abl<8, 2, 48, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 48)), KARGS))
+  ADD("tile16 consume interleaved", true, hipLaunchKernelGGL((lab::k_pipe_abl<8, 2, 16, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 16)), KARGS))
+  // lab8: no empty pass at a round's end (+ interleaved consume)
+  ADD("odd tail pass", true, hipLaunchKernelGGL((lab::k_pipe_abl<10, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
+  ADD("odd tail pass + consume interleaved", true, hipLaunchKernelGGL((lab::k_pipe_abl<11, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
+  // lab7: consume with the passes' scans interleaved
+  ADD("consume interleaved", true, hipLaunchKernelGGL((lab::k_pipe_abl<8, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   // lab6: per-chunk LDS atomics instead of the telescoping scan (u64 / low u32 word)
   ADD("direct atomics u64", true, hipLaunchKernelGGL((lab::k_pipe_abl<6, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   ADD("direct atomics u32", false, hipLaunchKernelGGL((lab::k_pipe_abl<7, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
