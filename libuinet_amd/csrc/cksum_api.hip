@@ -58,7 +58,7 @@ int check_launch() { return record_hip(hipGetLastError()); }
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_variant{0}, chains_pass{2}, host_threads{8},
       chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1}, walk_prefetch{1},
-      spans_contig{0}, spans_geo{0}, spans_sdesc{1};
+      spans_contig{0}, spans_geo{0}, spans_sdesc{1}, spans_pipe{1};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -81,6 +81,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"spans_contig", &TuningLive::spans_contig, [](int v) { return v == 0 || v == 1; }},
       {"spans_geo", &TuningLive::spans_geo, [](int v) { return v == 0 || span_geometry_ok(v); }},
       {"spans_sdesc", &TuningLive::spans_sdesc, [](int v) { return v == 0 || v == 1; }},
+      {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v == 0 || v == 1; }},
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
   };
   for (const Knob& k : knobs)
@@ -100,6 +101,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_SPANS_LUT", "spans_lut"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
         {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_CONTIG", "spans_contig"},
         {"UINET_CKSUM_SPANS_GEO", "spans_geo"},         {"UINET_CKSUM_SPANS_SDESC", "spans_sdesc"},
+        {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -107,7 +109,8 @@ static TuningLive& tuning_live() {
       int v = atoi(e);
       if (!strcmp(kv[1], "chains_variant") && e[0] == 's') v = 1;  // "serial"
       if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_lut") ||
-          !strcmp(kv[1], "spans_contig") || !strcmp(kv[1], "spans_sdesc"))
+          !strcmp(kv[1], "spans_contig") || !strcmp(kv[1], "spans_sdesc") ||
+          !strcmp(kv[1], "spans_pipe"))
         v = v ? 1 : 0;
       if (std::atomic<int>* f = tuning_field(*x, kv[1], v)) f->store(v, std::memory_order_relaxed);
     }
@@ -132,6 +135,7 @@ Tuning tuning() {
   x.spans_contig = ld(t.spans_contig);
   x.spans_geo = ld(t.spans_geo);
   x.spans_sdesc = ld(t.spans_sdesc);
+  x.spans_pipe = ld(t.spans_pipe);
   return x;
 }
 

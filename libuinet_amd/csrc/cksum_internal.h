@@ -24,6 +24,8 @@ struct Tuning {
   int spans_lut;       // span kernels: LDS mask table + one's-complement sums (0/1)
   int spans_contig;    // span kernels: block-contiguous packet ranges (0/1)
   int spans_sdesc;     // span kernels: per-wave scalar descriptor loads (0/1)
+  int spans_pipe;      // scalar-descriptor span kernels: persistent groups with two
+                       // packets in flight (k_spans_pp, 128 blocks per CU) (0/1)
   int spans_geo;       // span kernels: lanes-per-packet G and loads-per-lane U
                        // as G * 16 + U (0 = picked from the mean length)
   int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead, 2 lockstep chase

@@ -68,6 +68,22 @@ __device__ __forceinline__ void wave_desc(const uint64_t* __restrict__ off,
   }
 }
 
+// One u32 per packet (the seed) for the wave's kP packets, by scalar loads.
+template <int G>
+__device__ __forceinline__ uint32_t wave_u32(const uint32_t* __restrict__ a, uint32_t p,
+                                             uint32_t n) {
+  constexpr int kP = 64 / G;
+  const uint32_t gi = (threadIdx.x & 63) / G;
+  const uint32_t p0 = __builtin_amdgcn_readfirstlane(p - gi);
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < kP; ++k) {
+    const uint32_t v = __builtin_amdgcn_readfirstlane(sload32(a + min(p0 + (uint32_t)k, n - 1)));
+    if (gi == (uint32_t)k) r = v;
+  }
+  return r;
+}
+
 template <int G, int U, bool kStrided, bool kLut, bool kSDesc = false>
 __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ base,
                                                  const uint64_t* __restrict__ off,
@@ -145,6 +161,117 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
     a = base + o;
     sp.init(a, l);
     if (l) sp.load(0, gl);
+  }
+}
+
+// k_spans_pp: the scalar-descriptor span kernel with two packets in flight
+// per lane group.  Each group walks its packets p, p + S, p + 2S, ... (S the
+// grid's group count) with two register sets: packet k+1's chunks are loaded
+// before packet k is summed, so a group never waits between packets.  Every
+// load is unconditional (lanes past a span's end, and packets past the
+// group's end, re-load a chunk they already hold or the arena's first chunk,
+// and mask it away), so the compiler's wait for packet k counts packet
+// k+1's loads as still in flight.
+//
+// Why (profiles/r02/cold_ab/): with one packet per group the grid is 512
+// blocks per CU, and in the first launches after an idle gap (the power ramp
+// of a burst) such launches stretch from 0.21 to 0.32 ms for ~100 launches;
+// a pure streaming read does not, nor does a grid of 128 blocks per CU with 4
+// packets per group.  The driver's 5-warmup / 20-step window after a fresh
+// workload build: 0.70-0.85 of HBM peak one-shot, 0.88 with this kernel (3
+// boxes, 4 + 3 runs each).  Warm, back to back, the one-shot grid stays ~5 %
+// faster on config 2 (spans_pipe = 0 keeps it).
+template <int G, int U>
+struct SpanPP {
+  int head, end;  // the span's bytes are [head, end) from its first aligned chunk
+  u32x4 v[U];
+  // Loads the span's first G * U chunks (an empty span re-reads the arena's
+  // first chunk; lanes past the end re-read the last chunk) and keeps only
+  // what the fold needs.
+  __device__ __forceinline__ void load(const uint8_t* base, uint64_t o, uint32_t len, int gl) {
+    const uint8_t* a = base + o;
+    head = len ? (int)(reinterpret_cast<uintptr_t>(a) & 15) : 0;
+    end = head + (int)len;
+    const uint8_t* c0 = len ? a - head : base;
+    const uint32_t last = len ? ((uint32_t)(end + 15) >> 4) - 1u : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = load_chunk(c0 + 16u * min((uint32_t)(u * G + gl), last));
+  }
+  __device__ __forceinline__ uint32_t sum(const MaskLut& lut, int gl) const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = 16 * (u * G + gl);
+      acc += lut.sum_oc(v[u], head - b, end - b);
+    }
+    return acc;
+  }
+};
+
+template <int G, int U, bool kParity>
+__global__ __launch_bounds__(kBlock) void k_spans_pp(const uint8_t* __restrict__ base,
+                                                    const uint64_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ len,
+                                                    const uint32_t* __restrict__ seed,
+                                                    const uint8_t* __restrict__ parity,
+                                                    uint16_t* __restrict__ out, uint32_t n,
+                                                    uint32_t flags, uint32_t remap) {
+  static_assert(G >= 32, "scalar descriptors: one or two packets per wave");
+  constexpr uint32_t kGroups = kBlock / G;
+  constexpr int kChunks = G * U;
+  __shared__ MaskLut lut;
+  const int gl = threadIdx.x & (G - 1);
+  const uint32_t S = gridDim.x * kGroups;
+  const uint32_t lb = logical_block(remap);
+  uint32_t p = lb * kGroups + threadIdx.x / G;
+  // A packet's descriptors, fetched one packet ahead of its fold: off / len
+  // (and the seed) by scalar loads, the parity byte by a vector load.  No
+  // load sits under a branch, so the wait for a packet's chunks counts every
+  // later load as still in flight.
+  struct Desc {
+    uint64_t o;
+    uint32_t l, sd, lp;
+  };
+  auto desc = [&](uint32_t q) {
+    Desc d;
+    wave_desc<G>(off, len, q, n, d.o, d.l);
+    if (q >= n) d.l = 0;
+    d.sd = seed ? wave_u32<G>(seed, q, n) : 0u;  // uniform branch, scalar loads only
+    d.lp = kParity ? parity[min(q, n - 1)] : 0u;
+    return d;
+  };
+  // the packet's sum, stored; spans longer than G * U chunks finish with the
+  // serial rounds of Span (their later loads wait, as in k_spans)
+  auto done = [&](const SpanPP<G, U>& sp, uint32_t q, const Desc& d) {
+    uint64_t acc = sp.sum(lut, gl);
+    if (sp.end > 16 * kChunks) {
+      Span<G, U> rest;
+      rest.init(base + d.o, d.l);
+      acc += rest.rest_lut(lut, gl);
+    }
+    uint32_t x = fold16(acc);
+    if ((d.lp ^ (uint32_t)reinterpret_cast<uintptr_t>(base + d.o)) & 1) x = rot8(x);
+    x = group_sum<G>(x);
+    if (gl == 0 && q < n) out[q] = finish((uint64_t)x + d.sd, flags);
+  };
+  SpanPP<G, U> A, B;
+  Desc dA = desc(p);
+  A.load(base, dA.o, dA.l, gl);
+  lut.init();  // every thread reaches this barrier: no exit before it
+  if (__ballot(p < n) == 0) return;  // the whole wave is past the end
+  Desc dB = desc(p + S);
+  for (;;) {
+    B.load(base, dB.o, dB.l, gl);  // packet p + S in flight while p is summed
+    const Desc dC = desc(p + 2 * S);
+    done(A, p, dA);
+    if (__ballot(p + S < n) == 0) break;
+    A.load(base, dC.o, dC.l, gl);  // packet p + 2S in flight while p + S is summed
+    const Desc dD = desc(p + 3 * S);
+    done(B, p + S, dB);
+    if (__ballot(p + 2 * S < n) == 0) break;
+    p += 2 * S;
+    dA = dC;
+    dB = dD;
   }
 }
 
@@ -230,6 +357,25 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   // scalar at 256 / CU 0.2167, scalar at 512 / CU 0.2086 (+5.1 %), 4096 / CU
   // 0.2095; on a slower stretch of the same box +1.4 %.
   const bool sdesc = tuning().spans_sdesc && geo.g >= 32;
+  if (sdesc && tuning().spans_pipe) {
+    const int grid = grid_for(n, geo.g, 128);
+#define LP(G, U)                                                                          \
+  if (parity)                                                                             \
+    hipLaunchKernelGGL((k_spans_pp<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,      \
+                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
+                       flags, (uint32_t)tuning().xcd_remap);                               \
+  else                                                                                    \
+    hipLaunchKernelGGL((k_spans_pp<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,     \
+                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
+                       flags, (uint32_t)tuning().xcd_remap)
+    switch (geo.g * 16 + geo.u) {
+      case 32 * 16 + 3: LP(32, 3); break;
+      case 64 * 16 + 2: LP(64, 2); break;
+      default: LP(64, 3); break;
+    }
+#undef LP
+    return check_launch();
+  }
   const int grid = grid_for(n, geo.g, sdesc ? 512 : 256);
 #define L(G, U)                                                                          \
   if (sdesc && (G) >= 32)                                                                \

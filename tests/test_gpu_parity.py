@@ -108,6 +108,35 @@ def test_spans_contig_order(torch_dev, ora, n):
         u.set_tuning("spans_contig", 0)
 
 
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0)])
+def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
+    """The persistent two-in-flight span kernel (spans_pipe=1, the default
+    for 32 and 64 lanes per packet) and the one-packet-per-group kernel, on
+    grids small enough that every lane group walks many packets: ragged
+    batches, seeds, parity, UDP, spans longer than one round, empty spans."""
+    torch = torch_dev
+    rng = np.random.default_rng(700 + 10 * pipe + bpc)
+    arena = rand_arena(1 << 22, 41)
+    u.set_tuning("spans_pipe", pipe)
+    u.set_tuning("blocks_per_cu", bpc)
+    try:
+        for n in (1, 7, 6000, 70001):
+            off, ln = rand_spans(rng, n, arena.size, 12000)
+            seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+            par = rng.integers(0, 2, n).astype(np.uint8)
+            d = dict(arena=dev(torch, arena), off=dev(torch, off), ln=dev(torch, ln.astype(np.int32)))
+            for hint in (1500, 9000):
+                want = ora.spans(arena, off, ln, seed, par, u.F_UDP)
+                got = u.cksum_spans(d["arena"], d["off"], d["ln"], seed=dev(torch, seed.view(np.int32)),
+                                    parity=dev(torch, par), flags=u.F_UDP, len_hint=hint)
+                np.testing.assert_array_equal(host16(got), want)
+                got = u.cksum_spans(d["arena"], d["off"], d["ln"], len_hint=hint)
+                np.testing.assert_array_equal(host16(got), ora.spans(arena, off, ln))
+    finally:
+        u.set_tuning("spans_pipe", 1)
+        u.set_tuning("blocks_per_cu", 0)
+
+
 def test_spans_long(torch_dev, ora):
     """Spans far longer than one unrolled round of any geometry."""
     torch = torch_dev

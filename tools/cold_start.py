@@ -73,6 +73,7 @@ def main():
     ap.add_argument("--launches", type=int, default=400)
     ap.add_argument("--idle-s", type=float, default=1.0)
     ap.add_argument("--config", default="2")
+    ap.add_argument("--api", default="spans", help="spans | strided")
     a = ap.parse_args()
 
     sampler = ClockSampler()
@@ -87,7 +88,7 @@ def main():
     t_build0 = time.perf_counter() - sampler.t0
     w = bench.build_workload(a.config, None, 0)
     outs = [torch.empty(w["n"], dtype=torch.uint16, device="cuda") for _ in range(2)]
-    launches = [bench.make_launch(a.config, w, "spans", o) for o in outs]
+    launches = [bench.make_launch(a.config, w, a.api, o) for o in outs]
     s = torch.cuda.current_stream()
     torch.cuda.synchronize()
     t_build1 = time.perf_counter() - sampler.t0
@@ -106,7 +107,8 @@ def main():
         ms = np.array([e0.elapsed_time(e1) for e0, e1 in ev])
         return ms, t_start, t_end
 
-    res = {"workload": w["desc"], "bytes": w["bytes"], "build_s": [t_build0, t_build1]}
+    res = {"workload": w["desc"], "api": a.api, "bytes": w["bytes"],
+           "build_s": [t_build0, t_build1]}
     for phase in ("driver", "idle"):
         if phase == "idle":
             time.sleep(a.idle_s)

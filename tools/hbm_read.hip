@@ -6,6 +6,8 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
@@ -98,7 +100,43 @@ float time_it(F f, int reps) {
   return best;
 }
 
+// `hbm_read cold N`: after 2 s idle, N back-to-back launches of the best
+// pure-read shape (tile_u4, one tile per block) over config 2's 1.5 GB, each
+// bracketed by events -- the cold-start profile of a kernel with next to no
+// arithmetic, beside tools/cold_start.py's for the checksum kernels.
+static int cold(int n) {
+  const uint64_t bytes = 1572864000ull, n16 = bytes / 16;
+  uint4* p;
+  uint32_t* sink;
+  CK(hipMalloc(&p, bytes));
+  CK(hipMalloc(&sink, 64));
+  CK(hipMemset(p, 0x5a, bytes));
+  CK(hipDeviceSynchronize());
+  const int grid = (int)((n16 + 1023) / 1024);
+  k_read_tile<4, false><<<grid, 256>>>(p, n16, sink);  // first touch, untimed
+  CK(hipDeviceSynchronize());
+  usleep(2000000);
+  hipEvent_t* ev = (hipEvent_t*)malloc(sizeof(hipEvent_t) * (n + 1));
+  for (int i = 0; i <= n; ++i) CK(hipEventCreate(&ev[i]));
+  CK(hipEventRecord(ev[0]));
+  for (int i = 0; i < n; ++i) {
+    k_read_tile<4, false><<<grid, 256>>>(p, n16, sink);
+    CK(hipEventRecord(ev[i + 1]));
+  }
+  CK(hipEventSynchronize(ev[n]));
+  printf("{\"kernel\": \"tile_u4\", \"grid\": %d, \"bytes\": %llu, \"ms\": [", grid,
+         (unsigned long long)bytes);
+  for (int i = 0; i < n; ++i) {
+    float ms;
+    CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    printf("%s%.5f", i ? ", " : "", ms);
+  }
+  printf("]}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 2 && !strcmp(argv[1], "cold")) return cold(atoi(argv[2]));
   const uint64_t bytes = (argc > 1 ? strtoull(argv[1], 0, 0) : (1572864000ull));
   const uint64_t n16 = bytes / 16;
   uint4* p; uint32_t* sink;
