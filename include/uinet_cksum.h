@@ -155,9 +155,10 @@ int uinet_cksum_device_ok(void);
  *                     or one vector load per lane group (0)
  *   "spans_pipe"      scalar-descriptor span kernels: lane groups that walk
  *                     4+ packets each (128 blocks per CU) with two in flight
- *                     (1, default), or one packet per group (0: 512 blocks
- *                     per CU; ~5 % faster warm, up to 25 % slower in the
- *                     first launches after an idle gap)
+ *                     (1, default), one packet per group (0: 512 blocks per
+ *                     CU; ~5 % faster warm, up to 25 % slower in the first
+ *                     launches after an idle gap), or one wave per packet
+ *                     with scalar per-packet arithmetic (2)
  *   "spans_geo"       span kernels: force the lanes-per-packet G and loads
  *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
  *                     16x3, 32x3, 64x2, 64x3); 0 = picked from len_hint

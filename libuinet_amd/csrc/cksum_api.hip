@@ -81,7 +81,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"spans_contig", &TuningLive::spans_contig, [](int v) { return v == 0 || v == 1; }},
       {"spans_geo", &TuningLive::spans_geo, [](int v) { return v == 0 || span_geometry_ok(v); }},
       {"spans_sdesc", &TuningLive::spans_sdesc, [](int v) { return v == 0 || v == 1; }},
-      {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v == 0 || v == 1; }},
+      {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v >= 0 && v <= 2; }},
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
   };
   for (const Knob& k : knobs)
@@ -109,8 +109,7 @@ static TuningLive& tuning_live() {
       int v = atoi(e);
       if (!strcmp(kv[1], "chains_variant") && e[0] == 's') v = 1;  // "serial"
       if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_lut") ||
-          !strcmp(kv[1], "spans_contig") || !strcmp(kv[1], "spans_sdesc") ||
-          !strcmp(kv[1], "spans_pipe"))
+          !strcmp(kv[1], "spans_contig") || !strcmp(kv[1], "spans_sdesc"))
         v = v ? 1 : 0;
       if (std::atomic<int>* f = tuning_field(*x, kv[1], v)) f->store(v, std::memory_order_relaxed);
     }

@@ -23,6 +23,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "cksum_device.h"
 
 namespace uinet {
@@ -275,6 +277,117 @@ __global__ __launch_bounds__(kBlock) void k_spans_pp(const uint8_t* __restrict__
   }
 }
 
+// k_spans_w: one wave per packet, two packets in flight per wave, and every
+// per-packet quantity wave-uniform.  A packet's offset, length, seed and
+// chunk geometry are scalar loads and SALU arithmetic; its U * 64 chunk loads
+// take the scalar base plus a 32-bit lane offset; the 64 lane sums meet in a
+// DPP scan and the fold, rotation and complement run on the scalar unit.
+// About 29 VALU instructions per KiB against 47 for k_spans_pp and 66 for the
+// one-packet-per-group grid: under the power ramp of a burst the clock
+// holds (a streaming read with 64 integer multiply-adds per 16-B chunk dips
+// like the one-shot grid, one with 32 does not: profiles/r02/cold_ab/).
+template <int U, bool kParity>
+__global__ __launch_bounds__(kBlock) void k_spans_w(const uint8_t* __restrict__ base,
+                                                   const uint64_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ len,
+                                                   const uint32_t* __restrict__ seed,
+                                                   const uint8_t* __restrict__ parity,
+                                                   uint16_t* __restrict__ out, uint32_t n,
+                                                   uint32_t flags, uint32_t remap) {
+  constexpr int kChunks = 64 * U;
+  __shared__ MaskLut lut;
+  const int lane = threadIdx.x & 63;
+  constexpr uint32_t kWavesPB = kBlock / 64;
+  const uint32_t W = gridDim.x * kWavesPB;  // packets per round of the grid
+  const uint32_t p0 =
+      __builtin_amdgcn_readfirstlane(logical_block(remap) * kWavesPB + (threadIdx.x >> 6));
+  struct Desc {
+    const uint8_t* c0;  // first aligned chunk (the arena start for an empty span)
+    int head, end;      // the span is bytes [head, end) from c0
+    uint32_t last;      // its last chunk
+    uint32_t sd;        // seed
+    uint32_t lp;        // logical parity (a vector load, one packet ahead)
+    uint32_t odd;       // address parity of the span's first byte
+  };
+  auto desc = [&](uint32_t q) {
+    Desc d;
+    const uint32_t qc = min(q, n - 1);
+    const uint64_t o = sload64(off + qc);
+    const uint32_t l = q < n ? sload32(len + qc) : 0u;
+    const uint8_t* a = base + o;
+    d.head = l ? (int)(reinterpret_cast<uintptr_t>(a) & 15) : 0;
+    d.c0 = l ? a - d.head : base;
+    d.end = d.head + (int)l;
+    d.last = l ? ((uint32_t)(d.end + 15) >> 4) - 1u : 0u;
+    d.sd = seed ? sload32(seed + qc) : 0u;
+    d.lp = kParity ? parity[qc] : 0u;
+    d.odd = (uint32_t)reinterpret_cast<uintptr_t>(a) & 1u;
+    return d;
+  };
+  auto load = [&](const Desc& d, u32x4 (&v)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = load_chunk(d.c0 + 16u * min((uint32_t)(u * 64 + lane), d.last));
+  };
+  uint32_t res = 0, slot = 0;  // lane j: the result of packet p0 + j * W
+  auto done = [&](const Desc& d, const u32x4 (&v)[U]) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = 16 * (u * 64 + lane);
+      acc += lut.sum_oc(v[u], d.head - b, d.end - b);
+    }
+    uint64_t s64 = fold16_32(acc);
+    if (d.end > 16 * kChunks) {  // longer than one round: the rest as in k_spans
+      for (uint32_t k0 = kChunks; k0 <= d.last; k0 += kChunks) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          w[u] = load_chunk(d.c0 + 16u * min(k0 + (uint32_t)(u * 64 + lane), d.last));
+        uint32_t r = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int b = 16 * (int)(k0 + (uint32_t)(u * 64 + lane));
+          r += lut.sum_oc(w[u], d.head - b, d.end - b);
+        }
+        s64 += fold16_32(r);
+      }
+    }
+    // the wave's total, then the scalar unit's fold / rotation / complement
+    const uint32_t tot =
+        __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(s64), 0u), 63);  // < 2^22
+    uint32_t x = fold16_32(tot);
+    if ((d.lp ^ d.odd) & 1) x = rot8(x);
+    // results wait in lane `slot` of `res` and are stored after the loop (the
+    // host sizes the grid so that no wave folds more than 64 packets): a
+    // store inside the loop makes the next packet's loads wait for it
+    if (lane == (int)slot) res = finish((uint64_t)x + d.sd, flags);
+    ++slot;
+  };
+  u32x4 vA[U], vB[U];
+  Desc dA = desc(p0);
+  load(dA, vA);
+  lut.init();  // every thread reaches this barrier: no exit before it
+  if (p0 >= n) return;  // wave-uniform
+  uint32_t p = p0;
+  Desc dB = desc(p + W);
+  for (;;) {
+    load(dB, vB);  // packet p + W in flight while p is folded
+    const Desc dC = desc(p + 2 * W);
+    done(dA, vA);
+    if (p + W >= n) break;
+    load(dC, vA);  // packet p + 2W in flight while p + W is folded
+    const Desc dD = desc(p + 3 * W);
+    done(dB, vB);
+    if (p + 2 * W >= n) break;
+    p += 2 * W;
+    dA = dC;
+    dB = dD;
+  }
+  const uint32_t q = p0 + (uint32_t)lane * W;
+  if ((uint32_t)lane < slot && q < n) out[q] = (uint16_t)res;
+}
+
 struct Geometry {
   int g, u;
 };
@@ -357,6 +470,27 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   // scalar at 256 / CU 0.2167, scalar at 512 / CU 0.2086 (+5.1 %), 4096 / CU
   // 0.2095; on a slower stretch of the same box +1.4 %.
   const bool sdesc = tuning().spans_sdesc && geo.g >= 32;
+  if (sdesc && tuning().spans_pipe == 2) {
+    // one wave per packet: U loads per lane cover U * 64 chunks
+    const int u = len_hint <= 2032 ? 2 : 3;
+    // at most 64 packets per wave (its results are stored from one register)
+    const int grid = std::max<int>(grid_for(n, 64, 128), (int)(((uint64_t)n + 255) / 256));
+#define LW(U)                                                                             \
+  if (parity)                                                                             \
+    hipLaunchKernelGGL((k_spans_w<U, true>), dim3(grid), dim3(kBlock), 0, stream,          \
+                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
+                       flags, (uint32_t)tuning().xcd_remap);                               \
+  else                                                                                    \
+    hipLaunchKernelGGL((k_spans_w<U, false>), dim3(grid), dim3(kBlock), 0, stream,         \
+                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
+                       flags, (uint32_t)tuning().xcd_remap)
+    if (u == 2)
+      LW(2);
+    else
+      LW(3);
+#undef LW
+    return check_launch();
+  }
   if (sdesc && tuning().spans_pipe) {
     const int grid = grid_for(n, geo.g, 128);
 #define LP(G, U)                                                                          \

@@ -108,10 +108,11 @@ def test_spans_contig_order(torch_dev, ora, n):
         u.set_tuning("spans_contig", 0)
 
 
-@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0), (2, 1), (2, 0)])
 def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
     """The persistent two-in-flight span kernel (spans_pipe=1, the default
-    for 32 and 64 lanes per packet) and the one-packet-per-group kernel, on
+    for 32 and 64 lanes per packet), the wave-per-packet kernel (2) and the
+    one-packet-per-group kernel (0), on
     grids small enough that every lane group walks many packets: ragged
     batches, seeds, parity, UDP, spans longer than one round, empty spans."""
     torch = torch_dev

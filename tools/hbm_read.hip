@@ -100,6 +100,68 @@ float time_it(F f, int reps) {
   return best;
 }
 
+// Tile read with K dependent-free integer multiply-adds per 16-B chunk and
+// lane: the arithmetic load of a checksum kernel without its memory shape.
+template <int K>
+__global__ __launch_bounds__(256) void k_read_valu(const uint4* __restrict__ p, uint64_t n16,
+                                                   uint32_t* __restrict__ sink) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t tiles = (n16 + 1023) / 1024;
+  uint32_t acc0 = threadIdx.x, acc1 = 1, acc2 = 2, acc3 = 3;
+  for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t i = min(t * 1024 + (uint64_t)u * 256 + threadIdx.x, n16 - 1);
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + i));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int k = 0; k < K; k += 4) {
+        acc0 = acc0 * 3u + v[u].x;
+        acc1 = acc1 * 5u + v[u].y;
+        acc2 = acc2 * 7u + v[u].z;
+        acc3 = acc3 * 9u + v[u].w;
+      }
+      if (K == 0) acc0 += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+  }
+  if ((acc0 ^ acc1 ^ acc2 ^ acc3) == 0x12345678u) sink[0] = acc0;
+}
+
+template <int K>
+static int cold_valu(int n) {
+  const uint64_t bytes = 1572864000ull, n16 = bytes / 16;
+  uint4* p;
+  uint32_t* sink;
+  CK(hipMalloc(&p, bytes));
+  CK(hipMalloc(&sink, 64));
+  CK(hipMemset(p, 0x5a, bytes));
+  const int grid = (int)((n16 + 1023) / 1024);
+  k_read_valu<K><<<grid, 256>>>(p, n16, sink);
+  CK(hipDeviceSynchronize());
+  usleep(2000000);
+  hipEvent_t* ev = (hipEvent_t*)malloc(sizeof(hipEvent_t) * (n + 1));
+  for (int i = 0; i <= n; ++i) CK(hipEventCreate(&ev[i]));
+  CK(hipEventRecord(ev[0]));
+  for (int i = 0; i < n; ++i) {
+    k_read_valu<K><<<grid, 256>>>(p, n16, sink);
+    CK(hipEventRecord(ev[i + 1]));
+  }
+  CK(hipEventSynchronize(ev[n]));
+  printf("{\"kernel\": \"read_valu%d\", \"ms\": [", K);
+  for (int i = 0; i < n; ++i) {
+    float ms;
+    CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    printf("%s%.5f", i ? ", " : "", ms);
+  }
+  printf("]}\n");
+  CK(hipFree(p));
+  CK(hipFree(sink));
+  return 0;
+}
+
 // `hbm_read cold N`: after 2 s idle, N back-to-back launches of the best
 // pure-read shape (tile_u4, one tile per block) over config 2's 1.5 GB, each
 // bracketed by events -- the cold-start profile of a kernel with next to no
@@ -137,6 +199,11 @@ static int cold(int n) {
 
 int main(int argc, char** argv) {
   if (argc > 2 && !strcmp(argv[1], "cold")) return cold(atoi(argv[2]));
+  if (argc > 3 && !strcmp(argv[1], "cold_valu")) {
+    const int k = atoi(argv[3]), n = atoi(argv[2]);
+    return k >= 64 ? cold_valu<64>(n) : k >= 32 ? cold_valu<32>(n) : k >= 16 ? cold_valu<16>(n)
+                                                                            : cold_valu<0>(n);
+  }
   const uint64_t bytes = (argc > 1 ? strtoull(argv[1], 0, 0) : (1572864000ull));
   const uint64_t n16 = bytes / 16;
   uint4* p; uint32_t* sink;
