@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_pp(const uint8_t* __restrict__
 // chunk geometry are scalar loads and SALU arithmetic; its U * 64 chunk loads
 // take the scalar base plus a 32-bit lane offset; the 64 lane sums meet in a
 // DPP scan and the fold, rotation and complement run on the scalar unit.
-// About 29 VALU instructions per KiB against 47 for k_spans_pp and 66 for the
+// About 36 VALU instructions per KiB (ISA count) against 47 for k_spans_pp and ~66 for the
 // one-packet-per-group grid: under the power ramp of a burst the clock
 // holds (a streaming read with 64 integer multiply-adds per 16-B chunk dips
 // like the one-shot grid, one with 32 does not: profiles/r02/cold_ab/).
