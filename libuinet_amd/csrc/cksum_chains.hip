@@ -168,13 +168,13 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
   auto consume = [&](const u32x4 (&v)[kPass], const uint32_t (&key)[kPass]) {
     uint32_t P[kPass], sl[kPass], nx[kPass];
 #pragma unroll
-    for (int q = 0; q < kPass; ++q) P[q] = lut.sum_oc_idx(v[q], key[q] & 0xffffu);  // < 2^17
+    for (int q = 0; q < kPass; ++q) P[q] = lut.sum_oc_idx(v[q], key[q] & 0xffffu);  // < 2^19
 #pragma unroll
     for (int q = 0; q < kPass; ++q) {
       sl[q] = key[q] >> 16;
       nx[q] = wave_shl1(sl[q]);
     }
-    wave_scan_add_n<kPass>(P);  // < 2^23
+    wave_scan_add_n<kPass>(P);  // < 2^25
 #pragma unroll
     for (int q = 0; q < kPass; ++q) {
       if (lane == 63 || nx[q] != sl[q]) {
