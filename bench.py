@@ -322,8 +322,16 @@ def main():
     if distributed and backend == "nccl":
         # a non-blocking stream of its own for the kernels (made current, so
         # the collectives order themselves after it) instead of the null
-        # stream: 0.481 vs 0.489 ms per step at world 1 (profiles/r02/s3)
-        stream = torch.cuda.Stream()
+        # stream: 0.481 vs 0.489 ms per step at world 1 (profiles/r02/gather/).
+        # High priority: a hardware queue apart from RCCL's normal-priority
+        # stream, so that step k's gather kernel does not sit between the
+        # kernels of steps k + 1 and k + 2
+        stream = torch.cuda.Stream(priority=-1)
+        # it does not synchronise with the null stream: the workload's
+        # generation and descriptor uploads (null stream) must be complete
+        # before its first kernel reads them
+        stream.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
         torch.cuda.set_stream(stream)
     if args.desc == "packed" and args.config in CHAIN_CONFIGS:
         w["packed"] = u.pack_segments(w["seg_off"], w["seg_len"])
