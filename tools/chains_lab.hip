@@ -376,6 +376,10 @@ __global__ __launch_bounds__(kBlock) void k_grp(const uint8_t* __restrict__ base
 
 // k_chains_pipe with ablations: 1 = no chunk arithmetic / binning (bytes
 // xor-ed into a register), 2 = no loads, 3 = chunk sums but no binning.
+// tile timeline of the kAbl = 12 variant (set by the host in timeline mode)
+__device__ unsigned long long* g_ts;
+__device__ uint32_t g_q[256];  // kAbl = 13 / 19 work queues (zero at load time)
+
 template <int kAbl, int kPass, int kTile, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UINET_CHAINS_OCC void k_pipe_abl(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
@@ -390,13 +394,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
                 "a tile's packets are one per lane, lane kTile reads the end of its segment "
                 "range, and its 2 * kTile bins are one per lane");
   constexpr int kWin = 64 * kPass;  // chunks per batch of passes
+  constexpr int kWB = (kAbl == 16 || kAbl == 18) ? 1 : (kAbl == 17 ? 2 : kWaves);  // waves per block
   __shared__ MaskLut lut;
-  __shared__ unsigned long long lds_acc[kWaves][2 * kTile];  // (slot, rot) bins
-  __shared__ uint32_t lds_pkmark[kWaves][64];  // packet-start markers (slot + 1)
-  __shared__ uint8_t lds_mark[kWaves][kWin];   // segment-start markers (lane + 1)
+  __shared__ unsigned long long lds_acc[kWB][2 * kTile];  // (slot, rot) bins
+  __shared__ uint32_t lds_pkmark[kWB][64];  // packet-start markers (slot + 1)
+  __shared__ uint8_t lds_mark[kWB][kWin];   // segment-start markers (lane + 1)
   lut.init();
-  for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
-  for (int i = threadIdx.x; i < kWaves * kWin; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kWB * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kWB * kWin; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -404,7 +409,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
   uint32_t* pkmark = lds_pkmark[wid];
   uint8_t* mark = lds_mark[wid];
   const uint32_t tiles = (n + kTile - 1) / kTile;
-  const uint32_t wstride = gridDim.x * kWaves;
+  const uint32_t wstride = gridDim.x * kWB;
 
   // the pipeline's register sets: the pending batch (issued, not yet
   // consumed; `pend` wave-uniform) in a, the one being issued in b
@@ -414,7 +419,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
   uint32_t dummy = 0;
   auto consume = [&](const auto& v, const auto& key) {
     constexpr int NP = sizeof(key) / sizeof(key[0]);
-    if constexpr (kAbl == 8 || kAbl == 11) {
+    if constexpr (kAbl == 8 || kAbl == 11 || kAbl == 12 || kAbl == 13 || kAbl == 14 || kAbl == 15 || kAbl == 16 || kAbl == 17 || kAbl == 18 || kAbl == 19 || kAbl == 20) {
       // every pass's chunk sums first, then the passes' scans side by side
       // (independent DPP chains interleave), then the bin updates
       uint32_t P[NP], sl[NP], nx[NP];
@@ -449,9 +454,57 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
     }
   };
 
-  for (uint32_t t = blockIdx.x * kWaves + wid; t < tiles; t += wstride) {
-    const uint32_t P0 = t * kTile;
-    const int np = (int)min((uint32_t)kTile, n - P0);
+  // kAbl 13: tiles from a work queue (g_q[0]: next ticket, g_q[1]: waves
+  // done; the last wave out resets both for the next launch on the stream)
+  auto ticket = [&]() -> uint32_t {
+    uint32_t x = 0;
+    if (lane == 0) x = atomicAdd(&g_q[0], 1u);
+    return __builtin_amdgcn_readfirstlane(x);
+  };
+  uint32_t t_next = 0;
+  if constexpr (kAbl == 13) t_next = ticket();
+  // kAbl 14 / 15: wave gw of W owns the contiguous packets [gw n / W,
+  // (gw + 1) n / W) and walks them in tiles of kTile (15: + timeline)
+  const uint32_t gw = blockIdx.x * kWB + wid;
+  const uint32_t W = gridDim.x * kWB;
+  const uint32_t r_lo = (uint32_t)((uint64_t)gw * n / W);
+  const uint32_t r_hi = (uint32_t)((uint64_t)(gw + 1) * n / W);
+  constexpr bool kRange = kAbl == 14 || kAbl == 15;
+  // kAbl 19 / 20: 8 pools of tiles, one per XCD (workgroup i runs on XCD
+  // i mod 8); pool x's first kStatic % of tiles split into contiguous
+  // per-wave ranges, the rest taken one tile at a time from the pool's
+  // counter (g_q[32 x], own 128-B line); the wave that takes the pool's last
+  // failing ticket (one per pool wave) resets the counter. 20: + timeline.
+  constexpr bool kPool = kAbl == 19 || kAbl == 20;
+  constexpr uint32_t kStaticPct = 70;
+  const uint32_t px = blockIdx.x & 7u;
+  const uint32_t nbx = (gridDim.x + 7u - px) >> 3;  // blocks of pool px
+  const uint32_t Wx = nbx * kWB;
+  const uint32_t wx = (blockIdx.x >> 3) * kWB + wid;
+  const uint32_t p_lo = (uint32_t)((uint64_t)tiles * px / 8), p_hi = (uint32_t)((uint64_t)tiles * (px + 1) / 8);
+  const uint32_t S = (p_hi - p_lo) * kStaticPct / 100;
+  uint32_t s_cur = p_lo + (uint32_t)((uint64_t)S * wx / Wx);
+  const uint32_t s_end = p_lo + (uint32_t)((uint64_t)S * (wx + 1) / Wx);
+  auto pool_next = [&]() -> uint32_t {
+    if (s_cur < s_end) return s_cur++;
+    uint32_t x = 0;
+    if (lane == 0) {
+      x = atomicAdd(&g_q[32 * px], 1u);
+      const uint32_t dyn = p_hi - p_lo - S;
+      if (x == dyn + Wx - 1) atomicExch(&g_q[32 * px], 0u);  // the last ticket of this launch
+    }
+    x = __builtin_amdgcn_readfirstlane(x);
+    return x < p_hi - p_lo - S ? p_lo + S + x : 0xffffffffu;
+  };
+  uint32_t it = 0;
+  for (uint32_t t = kPool ? pool_next() : kRange ? r_lo : (kAbl == 13 ? t_next : blockIdx.x * kWB + wid);
+       kRange ? t < r_hi : t < tiles;
+       t = kPool ? pool_next() : kRange ? t + kTile : (kAbl == 13 ? t_next : t + wstride), ++it) {
+    if constexpr (kAbl == 13) t_next = ticket();  // one tile ahead
+    uint64_t t_begin = 0;
+    if constexpr (kAbl == 12 || kAbl == 15 || kAbl == 18 || kAbl == 20) t_begin = wall_clock64();
+    const uint32_t P0 = kRange ? t : t * kTile;
+    const int np = (int)min((uint32_t)kTile, (kRange ? r_hi : n) - P0);
     const uint32_t ps = pkt_seg[P0 + (uint32_t)min(lane, np)];
     const uint32_t k_skip = (lane < np && pskip) ? pskip[P0 + lane] : 0u;
     const uint32_t k_len = (lane < np) ? (plen ? plen[P0 + lane] : 0xffffffffu) : 0u;
@@ -674,6 +727,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
       out[p] = finish(acc[2 * lane] + rot8(odd) + (seed ? seed[p] : 0u) + (kAbl && kAbl != 4 && kAbl < 8 ? dummy : 0u), flags);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if constexpr (kAbl == 15) {
+      const uint64_t t_end = wall_clock64();
+      if (lane == 0 && it < 8) {
+        g_ts[3 * ((uint64_t)gw * 8 + it)] = t_begin;
+        g_ts[3 * ((uint64_t)gw * 8 + it) + 1] = t_end;
+        g_ts[3 * ((uint64_t)gw * 8 + it) + 2] = 1;
+      }
+    }
+    if constexpr (kAbl == 12 || kAbl == 18 || kAbl == 20) {
+      // tile timeline (100 MHz constant clock): begin, end, and HW_ID (which
+      // CU / SIMD / wave slot) -- vector stores from lane 0
+      const uint64_t t_end = wall_clock64();
+      if (lane == 0) {
+        g_ts[3 * (uint64_t)t] = t_begin;
+        g_ts[3 * (uint64_t)t + 1] = t_end;
+        g_ts[3 * (uint64_t)t + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+      }
+    }
+  }
+  if constexpr (kAbl == 13) {
+    if (lane == 0) {
+      const uint32_t d = atomicAdd(&g_q[1], 1u);
+      if (d == gridDim.x * kWB - 1) {  // every other wave has taken its last ticket
+        atomicExch(&g_q[0], 0u);
+        atomicExch(&g_q[1], 0u);
+      }
+    }
   }
 }
 
@@ -1072,14 +1152,74 @@ int main(int argc, char** argv) {
   const int rounds = argc > 2 ? atoi(argv[2]) : 8;
   const int launches = 20;
   Dev d = build_config3(n, 3);
+  if (const char* tl = getenv("LAB_TIMELINE")) {
+    // tile timeline of the shipped scheme (kAbl = 12: consume interleaved +
+    // timestamps): 10 warm launches, then the raw (begin, end, hw_id) per
+    // tile of one launch into the file named by LAB_TIMELINE
+    const int tl_grid0 = getenv("LAB_TL_GRID") ? atoi(getenv("LAB_TL_GRID")) : grid_for_tiles(d.n, 32);
+    const bool tl_range = getenv("LAB_TL_RANGE") != nullptr;
+    const uint32_t tiles = std::max<uint32_t>((d.n + 31) / 32, tl_range ? tl_grid0 * kWaves * 8 : 0);
+    unsigned long long* ts;
+    CK(hipMalloc(&ts, tiles * 24ull));
+    CK(hipMemset(ts, 0, tiles * 24ull));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(lab::g_ts), &ts, sizeof(ts)));
+    uint16_t* o;
+    CK(hipMalloc(&o, d.n * 2));
+    hipEvent_t a0, a1;
+    CK(hipEventCreate(&a0));
+    CK(hipEventCreate(&a1));
+    float ms = 0;
+    const int tl_grid = tl_grid0;
+    for (int r = 0; r < 11; ++r) {
+      CK(hipEventRecord(a0, 0));
+      if (getenv("LAB_TL_POOL"))
+        hipLaunchKernelGGL((lab::k_pipe_abl<20, 2, 32, uint64_t, uint32_t>), dim3(tl_grid),
+                           dim3(kBlock), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip,
+                           nullptr, o, d.n, 0u, 128u);
+      else if (getenv("LAB_TL_WPB1"))
+        hipLaunchKernelGGL((lab::k_pipe_abl<18, 2, 32, uint64_t, uint32_t>), dim3((d.n + 31) / 32),
+                           dim3(64), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip,
+                           nullptr, o, d.n, 0u, 128u);
+      else if (tl_range)
+        hipLaunchKernelGGL((lab::k_pipe_abl<15, 2, 32, uint64_t, uint32_t>), dim3(tl_grid),
+                           dim3(kBlock), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip,
+                           nullptr, o, d.n, 0u, 128u);
+      else
+        hipLaunchKernelGGL((lab::k_pipe_abl<12, 2, 32, uint64_t, uint32_t>), dim3(tl_grid),
+                           dim3(kBlock), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip,
+                           nullptr, o, d.n, 0u, 128u);
+      CK(hipEventRecord(a1, 0));
+      CK(hipEventSynchronize(a1));
+      CK(hipEventElapsedTime(&ms, a0, a1));
+    }
+    std::vector<unsigned long long> h(tiles * 3ull);
+    CK(hipMemcpy(h.data(), ts, tiles * 24ull, hipMemcpyDeviceToHost));
+    FILE* f = fopen(tl, "wb");
+    if (!f) return 1;
+    fwrite(h.data(), 8, h.size(), f);
+    fclose(f);
+    printf("{\"packets\": %u, \"tiles\": %u, \"grid\": %d, \"last_launch_ms\": %.5f}\n", d.n, tiles,
+           tl_grid, ms);
+    return 0;
+  }
   std::vector<Variant> vs;
   vs.push_back({"pipe<2,32> (shipped)", true, [](const Dev& d, uint16_t* o) {
                   launch_chains(d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip, nullptr,
                                 o, d.n, 0, 0, 0);
                 }});
   const char* only = getenv("LAB_ONLY");  // substring filter on variant names
+  auto want = [&](const char* name) {  // LAB_ONLY: comma-separated substrings
+    if (!only) return true;
+    std::string l(only);
+    for (size_t p = 0, q; p <= l.size(); p = q + 1) {
+      q = l.find(',', p);
+      if (q == std::string::npos) q = l.size();
+      if (q > p && strstr(name, l.substr(p, q - p).c_str())) return true;
+    }
+    return false;
+  };
 #define ADD(NAME, EXACT, ...)                                                 \
-  if (!only || strstr(NAME, only) || !vs.size())                              \
+  if (want(NAME) || !vs.size())                                               \
     vs.push_back({NAME, EXACT, [](const Dev& d, uint16_t* o) { __VA_ARGS__; }});
 #define KARGS                                                                   \
   dim3(kBlock), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip, nullptr, o, d.n, \
@@ -1107,6 +1247,21 @@ int main(int argc, char** argv) {
   // lab8: no empty pass at a round's end (+ interleaved consume)
   ADD("odd tail pass", true, hipLaunchKernelGGL((lab::k_pipe_abl<10, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   ADD("odd tail pass + consume interleaved", true, hipLaunchKernelGGL((lab::k_pipe_abl<11, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
+  // lab10: tiles from a work queue, resident grids of 6 / 12 / 24 blocks per CU
+  ADD("queue bpc6", true, hipLaunchKernelGGL((lab::k_pipe_abl<13, 2, 32, uint64_t, uint32_t>), dim3(256 * 6), KARGS))
+  ADD("queue bpc12", true, hipLaunchKernelGGL((lab::k_pipe_abl<13, 2, 32, uint64_t, uint32_t>), dim3(256 * 12), KARGS))
+  ADD("queue bpc24", true, hipLaunchKernelGGL((lab::k_pipe_abl<13, 2, 32, uint64_t, uint32_t>), dim3(256 * 24), KARGS))
+  ADD("queue bpc6 tile8", true, hipLaunchKernelGGL((lab::k_pipe_abl<13, 2, 8, uint64_t, uint32_t>), dim3(256 * 6), KARGS))
+  ADD("range bpc6", true, hipLaunchKernelGGL((lab::k_pipe_abl<14, 2, 32, uint64_t, uint32_t>), dim3(256 * 6), KARGS))
+  ADD("range bpc12", true, hipLaunchKernelGGL((lab::k_pipe_abl<14, 2, 32, uint64_t, uint32_t>), dim3(256 * 12), KARGS))
+  ADD("range bpc6 tile16", true, hipLaunchKernelGGL((lab::k_pipe_abl<14, 2, 16, uint64_t, uint32_t>), dim3(256 * 6), KARGS))
+  // lab11: one / two waves per block (a finished wave's slot is refilled at once)
+  ADD("wpb1", true, hipLaunchKernelGGL((lab::k_pipe_abl<16, 2, 32, uint64_t, uint32_t>), dim3((d.n + 31) / 32), dim3(64), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip, nullptr, o, d.n, 0u, 128u))
+  ADD("wpb2", true, hipLaunchKernelGGL((lab::k_pipe_abl<17, 2, 32, uint64_t, uint32_t>), dim3((d.n + 63) / 64), dim3(128), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip, nullptr, o, d.n, 0u, 128u))
+  // lab12: XCD pools, 70 % static ranges + per-pool tile counters
+  ADD("pool bpc6", true, hipLaunchKernelGGL((lab::k_pipe_abl<19, 2, 32, uint64_t, uint32_t>), dim3(256 * 6), KARGS))
+  ADD("pool bpc5", true, hipLaunchKernelGGL((lab::k_pipe_abl<19, 2, 32, uint64_t, uint32_t>), dim3(256 * 5), KARGS))
+  ADD("static bpc6", true, hipLaunchKernelGGL((lab::k_pipe_abl<8, 2, 32, uint64_t, uint32_t>), dim3(256 * 6), KARGS))
   // lab7: consume with the passes' scans interleaved
   ADD("consume interleaved", true, hipLaunchKernelGGL((lab::k_pipe_abl<8, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   // lab6: per-chunk LDS atomics instead of the telescoping scan (u64 / low u32 word)
