@@ -378,10 +378,11 @@ __global__ __launch_bounds__(kBlock) void k_grp(const uint8_t* __restrict__ base
 // xor-ed into a register), 2 = no loads, 3 = chunk sums but no binning.
 // tile timeline of the kAbl = 12 variant (set by the host in timeline mode)
 __device__ unsigned long long* g_ts;
+__device__ uint32_t g_bc[2][16 * 2048];  // kAbl 21 / 22 block counters, two sets
 __device__ uint32_t g_q[256];  // kAbl = 13 / 19 work queues (zero at load time)
 
 template <int kAbl, int kPass, int kTile, typename OffT, typename LenT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UINET_CHAINS_OCC void k_pipe_abl(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__((kAbl == 21 || kAbl == 22) ? 768 : kBlock) __attribute__((amdgpu_waves_per_eu(6))) UINET_CHAINS_OCC void k_pipe_abl(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
                                                        const LenT* __restrict__ seg_len,
                                                        const uint32_t* __restrict__ pkt_seg,
@@ -394,7 +395,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
                 "a tile's packets are one per lane, lane kTile reads the end of its segment "
                 "range, and its 2 * kTile bins are one per lane");
   constexpr int kWin = 64 * kPass;  // chunks per batch of passes
-  constexpr int kWB = (kAbl == 16 || kAbl == 18) ? 1 : (kAbl == 17 ? 2 : kWaves);  // waves per block
+  constexpr bool kBP = kAbl == 21 || kAbl == 22;
+  constexpr int kWB = (kAbl == 16 || kAbl == 18) ? 1 : (kAbl == 17 ? 2 : ((kAbl == 21 || kAbl == 22) ? 12 : kWaves));  // waves per block
   __shared__ MaskLut lut;
   __shared__ unsigned long long lds_acc[kWB][2 * kTile];  // (slot, rot) bins
   __shared__ uint32_t lds_pkmark[kWB][64];  // packet-start markers (slot + 1)
@@ -419,7 +421,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
   uint32_t dummy = 0;
   auto consume = [&](const auto& v, const auto& key) {
     constexpr int NP = sizeof(key) / sizeof(key[0]);
-    if constexpr (kAbl == 8 || kAbl == 11 || kAbl == 12 || kAbl == 13 || kAbl == 14 || kAbl == 15 || kAbl == 16 || kAbl == 17 || kAbl == 18 || kAbl == 19 || kAbl == 20) {
+    if constexpr (kAbl == 8 || kAbl == 11 || kAbl == 12 || kAbl == 13 || kAbl == 14 || kAbl == 15 || kAbl == 16 || kAbl == 17 || kAbl == 18 || kAbl == 19 || kAbl == 20 || kAbl == 21 || kAbl == 22) {
       // every pass's chunk sums first, then the passes' scans side by side
       // (independent DPP chains interleave), then the bin updates
       uint32_t P[NP], sl[NP], nx[NP];
@@ -475,6 +477,34 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
   // per-wave ranges, the rest taken one tile at a time from the pool's
   // counter (g_q[32 x], own 128-B line); the wave that takes the pool's last
   // failing ticket (one per pool wave) resets the counter. 20: + timeline.
+  // kAbl 21 / 22: blocks of 12 waves (two per CU), block b owns the contiguous
+  // tiles [b per, (b + 1) per) and its waves take them one at a time from the
+  // block's counter g_bc[par][16 b]; the counters alternate between two sets
+  // by launch parity (long_ch), and each launch zeroes the other set for the
+  // next one.  A wave whose block is exhausted takes tiles from the next
+  // kSteal blocks' counters.  22: + timeline.
+  constexpr int kSteal = 4;
+  const uint32_t par = long_ch & 1u;
+  const uint32_t G_ = gridDim.x;
+  const uint32_t per_blk = (tiles + G_ - 1) / G_;  // once, scalar
+  auto blk_lo = [&](uint32_t v) { return min(v * per_blk, tiles); };
+  auto bticket = [&](uint32_t v) -> uint32_t {  // wave-uniform
+    uint32_t x = 0;
+    if (lane == 0) x = atomicAdd(&g_bc[par][16 * v], 1u);
+    return __builtin_amdgcn_readfirstlane(x);
+  };
+  uint32_t victim = 0;  // 0: own block, j: block + j
+  auto bp_next = [&]() -> uint32_t {
+    while (victim <= (uint32_t)kSteal) {
+      uint32_t v = blockIdx.x + victim;
+      if (v >= G_) v -= G_;
+      const uint32_t lo = blk_lo(v), hi = blk_lo(v + 1);
+      const uint32_t k = bticket(v);
+      if (lo + k < hi) return lo + k;
+      ++victim;
+    }
+    return 0xffffffffu;
+  };
   constexpr bool kPool = kAbl == 19 || kAbl == 20;
   constexpr uint32_t kStaticPct = 70;
   const uint32_t px = blockIdx.x & 7u;
@@ -496,13 +526,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
     x = __builtin_amdgcn_readfirstlane(x);
     return x < p_hi - p_lo - S ? p_lo + S + x : 0xffffffffu;
   };
+  if constexpr (kBP) {  // the other set, for the next launch on this stream
+    if (threadIdx.x == 0)
+      for (uint32_t v = blockIdx.x; v < 2048u; v += G_) atomicExch(&g_bc[par ^ 1u][16 * v], 0u);
+  }
   uint32_t it = 0;
-  for (uint32_t t = kPool ? pool_next() : kRange ? r_lo : (kAbl == 13 ? t_next : blockIdx.x * kWB + wid);
+  uint32_t bp_t = 0;
+  if constexpr (kBP) bp_t = bp_next();
+  for (uint32_t t = kBP ? bp_t : kPool ? pool_next() : kRange ? r_lo : (kAbl == 13 ? t_next : blockIdx.x * kWB + wid);
        kRange ? t < r_hi : t < tiles;
-       t = kPool ? pool_next() : kRange ? t + kTile : (kAbl == 13 ? t_next : t + wstride), ++it) {
+       t = kBP ? bp_t : kPool ? pool_next() : kRange ? t + kTile : (kAbl == 13 ? t_next : t + wstride), ++it) {
     if constexpr (kAbl == 13) t_next = ticket();  // one tile ahead
+    if constexpr (kBP) bp_t = bp_next();  // one tile ahead
     uint64_t t_begin = 0;
-    if constexpr (kAbl == 12 || kAbl == 15 || kAbl == 18 || kAbl == 20) t_begin = wall_clock64();
+    if constexpr (kAbl == 12 || kAbl == 15 || kAbl == 18 || kAbl == 20 || kAbl == 22) t_begin = wall_clock64();
     const uint32_t P0 = kRange ? t : t * kTile;
     const int np = (int)min((uint32_t)kTile, (kRange ? r_hi : n) - P0);
     const uint32_t ps = pkt_seg[P0 + (uint32_t)min(lane, np)];
@@ -559,7 +596,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
       const uint32_t meta = (slot << 1) | rot;
       const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
       // --- long segments: one wave-wide span each -------------------------
-      const bool is_long = nch >= kListMax || (long_ch != 0 && nch >= long_ch);
+      const bool is_long = nch >= kListMax || (!kBP && long_ch != 0 && nch >= long_ch);
       for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
         const int s = (int)__builtin_ctzll(lm);
         // head and length read separately: a segment may hold up to 4 GiB,
@@ -735,7 +772,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) UIN
         g_ts[3 * ((uint64_t)gw * 8 + it) + 2] = 1;
       }
     }
-    if constexpr (kAbl == 12 || kAbl == 18 || kAbl == 20) {
+    if constexpr (kAbl == 12 || kAbl == 18 || kAbl == 20 || kAbl == 22) {
       // tile timeline (100 MHz constant clock): begin, end, and HW_ID (which
       // CU / SIMD / wave slot) -- vector stores from lane 0
       const uint64_t t_end = wall_clock64();
@@ -1172,7 +1209,12 @@ int main(int argc, char** argv) {
     const int tl_grid = tl_grid0;
     for (int r = 0; r < 11; ++r) {
       CK(hipEventRecord(a0, 0));
-      if (getenv("LAB_TL_POOL"))
+      static uint32_t tl_ep = 1000;
+      if (getenv("LAB_TL_BP"))
+        hipLaunchKernelGGL((lab::k_pipe_abl<22, 2, 32, uint64_t, uint32_t>), dim3(512),
+                           dim3(768), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip,
+                           nullptr, o, d.n, 0u, ++tl_ep);
+      else if (getenv("LAB_TL_POOL"))
         hipLaunchKernelGGL((lab::k_pipe_abl<20, 2, 32, uint64_t, uint32_t>), dim3(tl_grid),
                            dim3(kBlock), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip,
                            nullptr, o, d.n, 0u, 128u);
@@ -1261,6 +1303,9 @@ int main(int argc, char** argv) {
   // lab12: XCD pools, 70 % static ranges + per-pool tile counters
   ADD("pool bpc6", true, hipLaunchKernelGGL((lab::k_pipe_abl<19, 2, 32, uint64_t, uint32_t>), dim3(256 * 6), KARGS))
   ADD("pool bpc5", true, hipLaunchKernelGGL((lab::k_pipe_abl<19, 2, 32, uint64_t, uint32_t>), dim3(256 * 5), KARGS))
+  // lab13: 12-wave blocks, per-block tile ranges and counters, stealing at the end
+  ADD("bp12 x512", true, { static uint32_t ep = 0; ++ep; hipLaunchKernelGGL((lab::k_pipe_abl<21, 2, 32, uint64_t, uint32_t>), dim3(512), dim3(768), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip, nullptr, o, d.n, 0u, ep); })
+  ADD("bp12 x1024", true, { static uint32_t ep = 0; ++ep; hipLaunchKernelGGL((lab::k_pipe_abl<21, 2, 32, uint64_t, uint32_t>), dim3(1024), dim3(768), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip, nullptr, o, d.n, 0u, ep); })
   ADD("static bpc6", true, hipLaunchKernelGGL((lab::k_pipe_abl<8, 2, 32, uint64_t, uint32_t>), dim3(256 * 6), KARGS))
   // lab7: consume with the passes' scans interleaved
   ADD("consume interleaved", true, hipLaunchKernelGGL((lab::k_pipe_abl<8, 2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
