@@ -158,7 +158,8 @@ int uinet_cksum_device_ok(void);
  *                     (1, default), one packet per group (0: 512 blocks per
  *                     CU; ~5 % faster warm, up to 25 % slower in the first
  *                     launches after an idle gap), or one wave per packet
- *                     with scalar per-packet arithmetic (2)
+ *                     with scalar per-packet arithmetic (2); the strided
+ *                     API at 32 / 64 lanes per packet follows 1 and 0
  *   "spans_geo"       span kernels: force the lanes-per-packet G and loads
  *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
  *                     16x3, 32x3, 64x2, 64x3); 0 = picked from len_hint

@@ -210,14 +210,15 @@ struct SpanPP {
   }
 };
 
-template <int G, int U, bool kParity>
+template <int G, int U, bool kParity, bool kStrided = false>
 __global__ __launch_bounds__(kBlock) void k_spans_pp(const uint8_t* __restrict__ base,
                                                     const uint64_t* __restrict__ off,
                                                     const uint32_t* __restrict__ len,
                                                     const uint32_t* __restrict__ seed,
                                                     const uint8_t* __restrict__ parity,
                                                     uint16_t* __restrict__ out, uint32_t n,
-                                                    uint32_t flags, uint32_t remap) {
+                                                    uint32_t flags, uint32_t remap,
+                                                    uint64_t stride = 0, uint32_t slen = 0) {
   static_assert(G >= 32, "scalar descriptors: one or two packets per wave");
   constexpr uint32_t kGroups = kBlock / G;
   constexpr int kChunks = G * U;
@@ -236,7 +237,12 @@ __global__ __launch_bounds__(kBlock) void k_spans_pp(const uint8_t* __restrict__
   };
   auto desc = [&](uint32_t q) {
     Desc d;
-    wave_desc<G>(off, len, q, n, d.o, d.l);
+    if constexpr (kStrided) {  // the strided API: packet q at q * stride, slen bytes
+      d.o = (uint64_t)min(q, n - 1) * stride;
+      d.l = slen;
+    } else {
+      wave_desc<G>(off, len, q, n, d.o, d.l);
+    }
     if (q >= n) d.l = 0;
     d.sd = seed ? wave_u32<G>(seed, q, n) : 0u;  // uniform branch, scalar loads only
     d.lp = kParity ? parity[min(q, n - 1)] : 0u;
@@ -541,6 +547,23 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   geo = geometry_override(geo);
   // one packet per group suits long packets; small ones want groups that
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
+  if (geo.g >= 32 && tuning().spans_pipe == 1) {
+    // the persistent two-in-flight groups of k_spans_pp, descriptors from
+    // the stride: as for the span API, the one-shot grid (spans_pipe = 0)
+    // slows under the platform's power limit (profiles/r02/ab_strided_pp/)
+    const int grid = grid_for(n, geo.g, 128);
+#define LS(G, U)                                                                           \
+  hipLaunchKernelGGL((k_spans_pp<G, U, false, true>), dim3(grid), dim3(kBlock), 0, stream, \
+                     static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, out, n, \
+                     flags, (uint32_t)tuning().xcd_remap, pkt_stride, len)
+    switch (geo.g * 16 + geo.u) {
+      case 32 * 16 + 3: LS(32, 3); break;
+      case 64 * 16 + 2: LS(64, 2); break;
+      default: LS(64, 3); break;
+    }
+#undef LS
+    return check_launch();
+  }
   const int grid = grid_for(n, geo.g, len <= 96 ? 256 : 4096);
 #define L(G, U)                                                                         \
   if (tuning().spans_lut)                                                               \

@@ -138,6 +138,35 @@ def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
         u.set_tuning("blocks_per_cu", 0)
 
 
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0)])
+def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
+    """The strided API on the persistent two-in-flight kernel (spans_pipe=1,
+    32 / 64 lanes per packet) and on the one-shot kernel (0), with grids small
+    enough that every lane group walks many packets: packet lengths of one
+    round and of several, aligned and unaligned strides and bases, seeds and
+    UDP, ragged counts."""
+    torch = torch_dev
+    rng = np.random.default_rng(900 + 10 * pipe + bpc)
+    arena = rand_arena(24 << 20, 43)
+    d_arena = dev(torch, arena)
+    u.set_tuning("spans_pipe", pipe)
+    u.set_tuning("blocks_per_cu", bpc)
+    try:
+        for length, stride, base in ((1500, 1500, 0), (1500, 1514, 14), (1480, 1501, 3),
+                                     (9000, 9000, 0), (8980, 9017, 5), (2000, 2048, 1)):
+            for n in (1, 5, 2049):
+                n = min(n, (arena.size - base - length) // stride)
+                seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+                off = base + stride * np.arange(n, dtype=np.int64)
+                got = u.cksum_strided(d_arena[base:], stride, length, n,
+                                      seed=dev(torch, seed.view(np.int32)), flags=u.F_UDP)
+                want = ora.spans(arena, off, np.full(n, length, np.int64), seed, None, u.F_UDP)
+                np.testing.assert_array_equal(host16(got), want)
+    finally:
+        u.set_tuning("spans_pipe", 1)
+        u.set_tuning("blocks_per_cu", 0)
+
+
 def test_spans_long(torch_dev, ora):
     """Spans far longer than one unrolled round of any geometry."""
     torch = torch_dev

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--tail", type=int, default=10, help="launches in the tail rate")
+    ap.add_argument("--api", default="spans", choices=["spans", "strided"])
     ap.add_argument("--variants", nargs="+",
                     default=["", "blocks_per_cu=256", "blocks_per_cu=32", "pure-read"])
     a = ap.parse_args()
@@ -47,7 +48,7 @@ def main():
     w = bench.build_workload("2", None, 0)
     out = torch.empty(w["n"], dtype=torch.uint16, device="cuda")
     s = torch.cuda.current_stream()
-    spans = bench.make_launch("2", w, "spans", out)
+    spans = bench.make_launch("2", w, a.api, out)
     arena64 = w["arena"][: (w["arena"].numel() // 8) * 8].view(torch.int64)
     sink = torch.empty((), dtype=torch.int64, device="cuda")
     # the engine's defaults (cksum_api.hip TuningLive), restored before each variant
@@ -91,7 +92,7 @@ def main():
     for r in res.values():
         r["window_median"] = float(np.median(r["window_tbs"]))
         r["tail_median"] = float(np.median(r["tail_tbs"]))
-    print(json.dumps({"workload": w["desc"], "idle_s": a.idle_s, "results": res}))
+    print(json.dumps({"workload": w["desc"], "api": a.api, "idle_s": a.idle_s, "results": res}))
 
 
 if __name__ == "__main__":
