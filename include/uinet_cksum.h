@@ -137,8 +137,10 @@ int uinet_cksum_device_ok(void);
 
 /* Performance knobs (process-wide; they never change results):
  *   "blocks_per_cu"   grid-stride launch width, 0 = per-kernel default
- *   "chains_variant"  0 = pipelined chunk stream (default), 1 = serial walk
- *   "chains_pass"     passes per batch in the chain kernel: 2, 4
+ *   "chains_variant"  0 = pipelined chunk stream (default), 1 = serial walk,
+ *                     2 = chunk stream with a bitmap segment lookup
+ *   "chains_pass"     passes per batch in the chain kernel: 2, 4 (3 with
+ *                     chains_variant 2 only; otherwise 2)
  *   "chains_long"     chain segments of at least this many 16-B chunks are
  *                     streamed wave-wide; 0 = never, else >= 16 (default 128)
  *   "chains_tile"     packets per wave in the chain kernel: 0 = auto, 8, 32

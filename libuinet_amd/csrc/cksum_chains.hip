@@ -86,6 +86,7 @@ constexpr int kWaves = kBlock / 64;
 #endif
 constexpr int kLongU = UINET_CHAINS_LONGU;  // chunks in flight per lane on a long segment
 constexpr uint32_t kListMax = 1024;  // longest segment (chunks) the chunk list takes
+constexpr uint32_t kListMaxBm = 128;  // the same for the bitmap lookup (<= 127 words)
 
 // 16-B raw buffer load, non-temporal (aux bit 1), from a resource spanning
 // 4 GiB: one VGPR of offset instead of a 64-bit address per chunk.
@@ -127,7 +128,7 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 #define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(kPass == 2 ? 6 : 1)))
 #endif
 
-template <int kPass, int kTile, typename OffT, typename LenT>
+template <int kPass, int kTile, bool kBm, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
                                                        const LenT* __restrict__ seg_len,
@@ -144,16 +145,24 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
   __shared__ MaskLut lut;
   __shared__ unsigned long long lds_acc[kWaves][2 * kTile];  // (slot, rot) bins
   __shared__ uint32_t lds_pkmark[kWaves][64];  // packet-start markers (slot + 1)
-  __shared__ uint8_t lds_mark[kWaves][kWin];   // segment-start markers (lane + 1)
+  // kBm = false: segment-start markers (lane + 1) per batch;
+  // kBm = true: the round's segment starts as a bitmap over its chunk list
+  // (bit c of word c / 64), at most 64 * (kListMaxBm - 1) chunks
+  constexpr int kMarkB = kBm ? 1 : kWin;
+  constexpr int kBmWords = kBm ? (int)kListMaxBm : 1;
+  __shared__ uint8_t lds_mark[kWaves][kMarkB];
+  __shared__ unsigned long long lds_bm[kWaves][kBmWords];
   lut.init();
   for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
-  for (int i = threadIdx.x; i < kWaves * kWin; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kWaves * kMarkB; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kWaves * kBmWords; i += blockDim.x) (&lds_bm[0][0])[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   unsigned long long* acc = lds_acc[wid];
   uint32_t* pkmark = lds_pkmark[wid];
   uint8_t* mark = lds_mark[wid];
+  unsigned long long* bm = lds_bm[wid];
   const uint32_t tiles = (n + kTile - 1) / kTile;
   const uint32_t wstride = gridDim.x * kWaves;
 
@@ -240,7 +249,8 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint32_t meta = (slot << 1) | rot;
       const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
       // --- long segments: one wave-wide span each -------------------------
-      const bool is_long = nch >= kListMax || (long_ch != 0 && nch >= long_ch);
+      const bool is_long =
+          nch >= (kBm ? kListMaxBm : kListMax) || (long_ch != 0 && nch >= long_ch);
       for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
         const int s = (int)__builtin_ctzll(lm);
         // head and length read separately: a segment may hold up to 4 GiB,
@@ -293,9 +303,75 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint32_t dkr = (uint32_t)rel - 16u * cst;  // mod 2^32; + 16 c lands in range
       const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(base + (R0 - (1ull << 31)));
       uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the batch
+      // kBm: the list segments' records compacted to lanes 0..L-1 in list
+      // order (ds_permute; the other lanes park theirs in L..63), the bitmap
+      // of their start chunks built by LDS atomics, 64 of its words held one
+      // per lane.  A chunk's segment is then the number of starts at or
+      // before it: two readlanes and an mbcnt per pass, no LDS round trip.
+      uint32_t cA = recA, cB = recB, cD0 = 0, cD1 = 0;
+      uint64_t bmw = 0;
+      uint32_t segc = 0;  // list segments started before the batch
+      if constexpr (kBm) {
+        if (nch_l != 0) atomicOr(&bm[cst >> 6], 1ull << (cst & 63u));
+        const uint32_t lrank = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(lm_list >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm_list, 0u));
+        const int dst = 4 * (nch_l != 0 ? (int)lrank : 63 - (lane - (int)lrank));
+        cA = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)recA);
+        cB = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)recB);
+        if (window) {
+          cD0 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)dkr);
+        } else {
+          cD0 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)dk);
+          cD1 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(dk >> 32));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        bmw = bm[lane];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        bm[lane] = 0;
+      }
       // Issue the batch at list chunk b into (v, key): segment lookup, mask
       // index and bin, loads.  Nothing here waits for packet bytes.
       auto issue = [&](uint32_t b, u32x4 (&v)[kPass], uint32_t (&key)[kPass], auto kWindow) {
+        if constexpr (kBm) {
+          if (b != 0 && (b & 4095u) == 0) {  // words 64..: lists of more than 4096 chunks
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            bmw = bm[(b >> 6) + (uint32_t)lane];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            bm[(b >> 6) + (uint32_t)lane] = 0;
+          }
+#pragma unroll
+          for (int q = 0; q < kPass; ++q) {
+            const int j = (int)(((b >> 6) + (uint32_t)q) & 63u);
+            const uint64_t M =
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bmw >> 32), j) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bmw, j);
+            // starts at or before the lane's chunk: bit 0, plus the bits of
+            // M >> 1 below the lane (mbcnt counts the bits below the lane)
+            const uint64_t Mr = M >> 1;
+            const int seg = (int)__builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(Mr >> 32),
+                __builtin_amdgcn_mbcnt_lo((uint32_t)Mr, segc + (uint32_t)(M & 1u) - 1u));
+            segc += (uint32_t)__builtin_popcountll(M);
+            const uint32_t c = b + (uint32_t)(q * 64 + lane);
+            const bool in = c < C;
+            const uint32_t cc = in ? c : C - 1;
+            const uint32_t a = (uint32_t)__shfl(cA, seg);
+            const uint32_t bq = (uint32_t)__shfl(cB, seg);
+            const int base16 = 16 * (int)c;
+            const int s_lo = (int)(a & 0xfffffu) - base16;
+            const int s_hi = in ? (int)bq - base16 : s_lo;
+            key[q] = MaskLut::index(s_lo, s_hi) | ((a >> 20) << 16);
+            if constexpr (decltype(kWindow)::value) {
+              const uint32_t d = (uint32_t)__shfl(cD0, seg);
+              v[q] = load_chunk_buf(rsrc, d + 16u * cc);
+            } else {
+              const uint32_t lo32 = (uint32_t)__shfl(cD0, seg);
+              const uint32_t hi32 = (uint32_t)__shfl(cD1, seg);
+              v[q] = load_chunk(base + ((((uint64_t)hi32 << 32) | lo32) + 16ull * cc));
+            }
+          }
+          return;
+        }
         const bool mk = nch_l != 0 && cst >= b && cst < b + kWin;
         if (mk) mark[cst - b] = (uint8_t)(lane + 1);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -419,19 +495,28 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
-#define LF(P, T)                                                                            \
-  hipLaunchKernelGGL((k_chains_pipe<P, T, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, b,    \
-                     seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
+#define LF(P, T, BM)                                                                          \
+  hipLaunchKernelGGL((k_chains_pipe<P, T, BM, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, \
+                     b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
+  const bool bmv = tn.chains_variant == 2;
   if (tile == 8) {
     if (tn.chains_pass == 4)
-      LF(4, 8);
+      LF(4, 8, false);
+    else if (bmv)
+      LF(2, 8, true);
     else
-      LF(2, 8);
+      LF(2, 8, false);
   } else {
-    if (tn.chains_pass == 4)
-      LF(4, 32);
+    if (bmv && tn.chains_pass == 3)
+      LF(3, 32, true);
+    else if (bmv && tn.chains_pass == 4)
+      LF(4, 32, true);
+    else if (tn.chains_pass == 4)
+      LF(4, 32, false);
+    else if (bmv)
+      LF(2, 32, true);
     else
-      LF(2, 32);
+      LF(2, 32, false);
   }
 #undef LF
   return check_launch();

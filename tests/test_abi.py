@@ -111,11 +111,11 @@ def test_set_tuning_validation():
     """uinet_cksum_set_tuning accepts each documented knob's range and rejects
     unknown keys and out-of-range values (no device needed)."""
     L = u.lib()
-    ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_variant", 1),
+    ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_variant", 1), ("chains_variant", 2),
           ("chains_pass", 4), ("chains_long", 0), ("chains_long", 16), ("chains_tile", 8),
           ("xcd_remap", 0), ("spans_lut", 1), ("host_threads", 64), ("walk_prefetch", 0),
           ("walk_prefetch", 2), ("spans_contig", 1), ("spans_geo", 0), ("spans_geo", 32 * 16 + 3), ("spans_sdesc", 0)]
-    bad = [("blocks_per_cu", -1), ("chains_variant", 2), ("chains_pass", 8), ("chains_long", 15),
+    bad = [("blocks_per_cu", -1), ("chains_variant", 3), ("chains_pass", 8), ("chains_long", 15),
            ("chains_tile", 64), ("xcd_remap", 2), ("host_threads", 0), ("walk_prefetch", 3),
            ("spans_contig", 2), ("spans_geo", 16 * 16 + 6), ("spans_geo", 5), ("spans_sdesc", 2), ("no_such_knob", 1)]
     try:

@@ -617,10 +617,12 @@ def test_zero_copy_pipeline_ring(torch_dev, ora, host_threads):
         np.testing.assert_array_equal(got[("hdr", k)], want_hdr)
 
 
+@pytest.mark.parametrize("variant", [0, 2])
 @pytest.mark.parametrize("long_ch,tile", [(0, 32), (16, 8), (16, 32), (64, 0), (200, 8)])
-def test_chains_long_segments(torch_dev, ora, long_ch, tile):
+def test_chains_long_segments(torch_dev, ora, long_ch, tile, variant):
     """Chains mixing short and long (wave-streamed) segments, with len/skip
-    clipping that cuts into long segments, over both tile sizes."""
+    clipping that cuts into long segments, over both tile sizes and both
+    segment lookups of the chunk-stream kernel."""
     torch = torch_dev
     rng = np.random.default_rng(5100 + long_ch + tile)
     arena = rand_arena(1 << 23, 51)
@@ -637,6 +639,7 @@ def test_chains_long_segments(torch_dev, ora, long_ch, tile):
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
     u.set_tuning("chains_long", long_ch)
     u.set_tuning("chains_tile", tile)
+    u.set_tuning("chains_variant", variant)
     try:
         for flags in (0, u.F_UDP):
             w = want if flags == 0 else ora.chains(arena, seg_off, seg_len, pkt_seg, length=length,
@@ -651,12 +654,51 @@ def test_chains_long_segments(torch_dev, ora, long_ch, tile):
     finally:
         u.set_tuning("chains_long", 128)
         u.set_tuning("chains_tile", 0)
+        u.set_tuning("chains_variant", 0)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("long_ch", [0, 200])
+def test_chains_full_rounds(torch_dev, ora, long_ch, variant):
+    """Descriptor rounds whose chunk list is longer than 4096 chunks: 64
+    segments of 1900-2031 B each (up to 127 chunks, the most a list segment
+    of the bitmap lookup holds), so the lookup crosses its 64-word bitmap
+    window; mixed with rounds of tiny and empty segments."""
+    torch = torch_dev
+    rng = np.random.default_rng(6100 + long_ch + variant)
+    arena = rand_arena(1 << 24, 61)
+    n = 2048
+    nseg = rng.integers(1, 9, n)
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    big = (np.arange(s) // 256) % 2 == 0
+    seg_len = np.where(big, rng.integers(1900, 2032, s), rng.integers(0, 40, s))
+    seg_off = rng.integers(0, arena.size - 2100, s).astype(np.int64)
+    tot = np.add.reduceat(seg_len, pkt_seg[:-1])
+    skip = np.where(rng.random(n) < 0.5, 20, (rng.random(n) * tot * 0.5).astype(np.int64))
+    length = np.where(rng.random(n) < 0.7, tot, skip + (rng.random(n) * (tot - skip + 1)).astype(np.int64))
+    want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip)
+    u.set_tuning("chains_long", long_ch)
+    u.set_tuning("chains_variant", variant)
+    u.set_tuning("chains_tile", 32)  # 32 packets x ~5 segments: full 64-segment rounds
+    try:
+        got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off),
+                             dev(torch, seg_len.astype(np.int32)),
+                             dev(torch, pkt_seg.astype(np.int32)),
+                             length=dev(torch, length.astype(np.int32)),
+                             skip=dev(torch, skip.astype(np.int32)), len_hint=1000)
+        np.testing.assert_array_equal(host16(got), want)
+    finally:
+        u.set_tuning("chains_long", 128)
+        u.set_tuning("chains_variant", 0)
+        u.set_tuning("chains_tile", 0)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_chains_kernel_variants(torch_dev, ora, variant):
-    """Both chain kernels (0 pipelined chunk stream, 1 serial walk) on chains
-    of 0..150 segments with len/skip/seed and the UDP flag."""
+    """The chain kernels (0 chunk stream, 1 serial walk, 2 chunk stream with
+    the bitmap segment lookup) on chains of 0..150 segments with
+    len/skip/seed and the UDP flag."""
     torch = torch_dev
     rng = np.random.default_rng(8800 + variant)
     arena = rand_arena(1 << 21, 47)
@@ -712,7 +754,7 @@ def test_chains_beyond_4gib_window(torch_dev, ora):
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     skip = np.full(n, 3, np.int64)
     want = ora.chains(host, seg_off, seg_len, pkt_seg, skip=skip, seed=seed)
-    for variant in (0, 1):
+    for variant in (0, 1, 2):
         u.set_tuning("chains_variant", variant)
         try:
             got = u.cksum_chains(d, dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
