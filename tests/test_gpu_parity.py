@@ -167,6 +167,38 @@ def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
         u.set_tuning("blocks_per_cu", 0)
 
 
+def test_spans_small_packets(torch_dev, ora):
+    """The small-packet geometries (4, 8 and 16 lanes per packet): ragged
+    counts, spans longer than the geometry's round, empty spans, seeds,
+    parity, UDP; the strided API at 64-B packets, 16-B aligned and not."""
+    torch = torch_dev
+    rng = np.random.default_rng(1300)
+    arena = rand_arena(24 << 20, 45)
+    d_arena = dev(torch, arena)
+    for hint, max_len in ((64, 80), (90, 120), (200, 300), (600, 900)):
+        for n in (1, 63, 64, 65, 1000, 70001):
+            # offsets leave room for the 5000-B spans (longer than the
+            # geometry's round) that 1 % of the packets get
+            off, ln = rand_spans(rng, n, arena.size - 5000, max_len)
+            ln[rng.random(n) < 0.01] = 5000
+            seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+            par = rng.integers(0, 2, n).astype(np.uint8)
+            d_off, d_ln = dev(torch, off), dev(torch, ln.astype(np.int32))
+            got = u.cksum_spans(d_arena, d_off, d_ln, seed=dev(torch, seed.view(np.int32)),
+                                parity=dev(torch, par), flags=u.F_UDP, len_hint=hint)
+            np.testing.assert_array_equal(host16(got), ora.spans(arena, off, ln, seed, par, u.F_UDP))
+            got = u.cksum_spans(d_arena, d_off, d_ln, len_hint=hint)
+            np.testing.assert_array_equal(host16(got), ora.spans(arena, off, ln))
+    for length, stride, base in ((64, 64, 0), (64, 80, 16), (60, 67, 3), (40, 64, 2)):
+        for n in (1, 65, 100003):
+            seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+            off = base + stride * np.arange(n, dtype=np.int64)
+            got = u.cksum_strided(d_arena[base:], stride, length, n,
+                                  seed=dev(torch, seed.view(np.int32)), flags=u.F_UDP)
+            want = ora.spans(arena, off, np.full(n, length, np.int64), seed, None, u.F_UDP)
+            np.testing.assert_array_equal(host16(got), want)
+
+
 def test_spans_long(torch_dev, ora):
     """Spans far longer than one unrolled round of any geometry."""
     torch = torch_dev
