@@ -95,7 +95,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rsrc(const uint8_t* sba
                                            0x00020000);
 }
 __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+#ifdef UINET_CHAINS_LAB_NOLOAD  // tools/chains_lab ablation only: no packet-byte loads
+  (void)r;
+  return u32x4{off, off ^ 0x5a5a5a5au, off + 7u, off * 3u};
+#else
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2);
+#endif
 }
 
 // k_chains_pipe: the pipelining and addressing details.
