@@ -130,6 +130,37 @@ def test_c_consumer_without_gpu(tmp_path, arena, golden):
     np.testing.assert_array_equal(got32, want32)
 
 
+def test_percall_fold_sanitized(tmp_path, arena, golden):
+    """The per-call fold (csrc/cksum_percall.cpp) built with AddressSanitizer
+    and UndefinedBehaviorSanitizer into the same C consumer, linked through
+    a test-only shim instead of the HIP library: every golden chain, pseudo
+    header and IP header, with no out-of-piece read, unaligned-access UB or
+    overflow reported, and the golden results."""
+    flags = ["-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+             "-fno-omit-frame-pointer", "-I", os.path.join(REPO, "include"),
+             "-I", os.path.join(REPO, "libuinet_amd", "csrc")]
+    objs = []
+    for cc, std, src in (("gcc", "-std=c11", "tests/native/percall_golden.c"),
+                         ("g++", "-std=c++17", "libuinet_amd/csrc/cksum_percall.cpp"),
+                         ("g++", "-std=c++17", "tests/native/percall_shim.cpp")):
+        o = tmp_path / (os.path.basename(src) + ".o")
+        subprocess.run([cc, std, *flags, "-c", os.path.join(REPO, src), "-o", str(o)], check=True)
+        objs.append(str(o))
+    exe = tmp_path / "percall_san"
+    subprocess.run(["g++", "-fsanitize=address,undefined", *objs, "-o", str(exe)], check=True)
+    inp = tmp_path / "in.bin"
+    want16, want32 = _write_input(str(inp), arena, golden)
+    # verify_asan_link_order=0: the environment may preload a library of its own
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe), str(inp)], capture_output=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert b"runtime error" not in r.stderr, r.stderr.decode()[-3000:]
+    n16 = want16.size
+    np.testing.assert_array_equal(np.frombuffer(r.stdout[: 2 * n16], np.uint16), want16)
+    np.testing.assert_array_equal(np.frombuffer(r.stdout[2 * n16:], np.uint32), want32)
+
+
 @pytest.mark.parametrize("length", [0, 1, 19, 20, 21, 1500, 65535])
 def test_per_call_edge_lengths(ora, length):
     arena = aligned_empty(70000)
