@@ -185,6 +185,24 @@ def load_traffic(path: str, key: str):
         return None
 
 
+def layout_floor_line(cfg: str, w, desc: str, kms) -> dict:
+    """Chain configs: the layout's HBM-traffic floor (distinct 128-B lines
+    holding a summed byte + the descriptors the kernel reads) and the kernel's
+    rate measured against it, beside the algorithmic roofline."""
+    import libuinet_amd.workloads as W
+
+    lay = w["layout"]
+    skip = lay.get("skip")
+    if skip is None:  # config 3: in_cksum_skip(m, len, 20)
+        skip = np.full(w["n"], 20, np.int64)
+    fl = W.layout_floor(lay["seg_off"], lay["seg_len"], lay["pkt_seg"], lay["lens"], skip,
+                        w.get("seed") is not None, 128, 6 if desc == "packed" else 12)
+    achieved = fl["floor_bytes"] / (float(kms.mean()) * 1e-3) / 1e9
+    return {"bytes": fl["floor_bytes"], "line": 128,
+            "over_algorithmic": round(fl["floor_bytes"] / w["bytes"], 4),
+            "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4)}
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -445,6 +463,8 @@ def main():
                 "kernel_ms_min": round(float(kms.min()), 5),
             },
         }
+        if args.config in CHAIN_CONFIGS:
+            result["roofline"]["layout_floor"] = layout_floor_line(args.config, w, args.desc, kms)
         if args.host_path:
             result["host_resident"] = host_path_rate(args, w)
     if world == 1 and rank == 0 and args.cpu_baseline == "auto":

@@ -301,3 +301,50 @@ def materialize_device(lay, device="cuda"):
                 seed=None if lay["seed"] is None else t(lay["seed"].view(np.int32), np.int32),
                 n=lay["n"], nseg=nseg, mean_seg=int(lay["seg_len"].sum() // max(1, nseg)),
                 bytes=lay["bytes"], layout=lay)
+
+
+def clipped_segments(seg_off, seg_len, pkt_seg, lens, skip):
+    """Per segment, the arena bytes [start, end) that in_cksum_skip(m, len,
+    skip) sums (in_cksum.c:203-229: len counts from the chain start), for the
+    segments that contribute; and the algorithmic byte count."""
+    seg_off, seg_len = np.asarray(seg_off, np.int64), np.asarray(seg_len, np.int64)
+    pkt_seg = np.asarray(pkt_seg, np.int64)
+    n = pkt_seg.size - 1
+    seg_pkt = np.repeat(np.arange(n), np.diff(pkt_seg))
+    run = np.cumsum(seg_len) - seg_len                      # running position over all chains
+    pos = run - run[np.minimum(pkt_seg[:-1], max(run.size - 1, 0))][seg_pkt]  # within its chain
+    lens = np.full(n, np.iinfo(np.int64).max) if lens is None else np.asarray(lens, np.int64)
+    skip = np.zeros(n, np.int64) if skip is None else np.asarray(skip, np.int64)
+    lo = np.clip(skip[seg_pkt] - pos, 0, seg_len)
+    hi = np.clip(lens[seg_pkt] - pos, 0, seg_len)
+    keep = hi > lo
+    return seg_off[keep] + lo[keep], seg_off[keep] + hi[keep], int((hi - lo)[keep].sum())
+
+
+def lines_touched(a, b, line: int) -> int:
+    """Distinct `line`-byte lines holding at least one byte of the [a, b) ranges."""
+    if a.size == 0:
+        return 0
+    first, last = a // line, (b - 1) // line
+    order = np.argsort(first, kind="stable")
+    f, l = first[order], last[order]
+    runmax = np.maximum.accumulate(l)
+    new = np.concatenate([[True], f[1:] > runmax[:-1]])
+    starts = f[new]
+    ends = np.maximum.reduceat(l, np.flatnonzero(new))
+    return int((ends - starts + 1).sum())
+
+
+def layout_floor(seg_off, seg_len, pkt_seg, lens, skip, seed: bool, line: int = 128,
+                 seg_desc_bytes: int = 12) -> dict:
+    """HBM-traffic floor of a chained batch: the distinct lines holding a
+    summed byte plus the descriptors the chain kernel reads (seg_desc_bytes
+    per segment: 12 wide, 6 packed; pkt_seg + len + skip [+ seed] per
+    packet).  What no kernel reading these packets from this layout can
+    avoid fetching."""
+    s, e, algo = clipped_segments(seg_off, seg_len, pkt_seg, lens, skip)
+    nseg, npkt = int(np.asarray(seg_len).size), int(np.asarray(pkt_seg).size) - 1
+    arena = lines_touched(s, e, line) * line
+    desc = seg_desc_bytes * nseg + npkt * (4 + 4 + 4 + (4 if seed else 0)) + 4
+    return dict(line=line, arena_bytes=arena, descriptor_bytes=desc, floor_bytes=arena + desc,
+                algorithmic_bytes=algo)

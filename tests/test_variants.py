@@ -95,3 +95,30 @@ def test_full_config3tx(torch_dev, ora):
 @pytest.mark.gpu
 def test_full_config5tso(torch_dev, ora):
     _gpu_vs_oracle(config5tso_layout(1111), ora)
+
+
+def test_layout_floor_small_cases():
+    """workloads.layout_floor on hand-checked chains: clipping to [skip, len)
+    counted from the chain start, shared and straddled lines, empty
+    contributions, descriptor bytes."""
+    import libuinet_amd.workloads as W
+
+    # packet 0: segments [0, 100) + [130, 330), len 300, skip 20 -> bytes
+    # [20, 100) and [130, 330); packet 1: segment [1000, 1040), whole chain
+    seg_off = np.array([0, 130, 1000], np.int64)
+    seg_len = np.array([100, 200, 40], np.int64)
+    pkt_seg = np.array([0, 2, 3], np.int64)
+    lens = np.array([300, 40], np.int64)
+    skip = np.array([20, 0], np.int64)
+    s, e, algo = W.clipped_segments(seg_off, seg_len, pkt_seg, lens, skip)
+    assert s.tolist() == [20, 130, 1000] and e.tolist() == [100, 330, 1040]
+    assert algo == 80 + 200 + 40
+    # 128-B lines: [20, 100) -> 0; [130, 330) -> 1, 2; [1000, 1040) -> 7, 8
+    f = W.layout_floor(seg_off, seg_len, pkt_seg, lens, skip, False, 128)
+    assert f["arena_bytes"] == 5 * 128
+    assert f["descriptor_bytes"] == 12 * 3 + 2 * 12 + 4
+    assert f["floor_bytes"] == f["arena_bytes"] + f["descriptor_bytes"]
+    # len cutting a chain short: packet 0 stops inside its first segment
+    s, e, algo = W.clipped_segments(seg_off, seg_len, pkt_seg, np.array([60, 40]), skip)
+    assert s.tolist() == [20, 1000] and e.tolist() == [60, 1040] and algo == 80
+    assert W.lines_touched(np.array([0, 64]), np.array([64, 65]), 64) == 2

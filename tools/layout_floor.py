@@ -20,30 +20,6 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def clipped_segments(seg_off, seg_len, pkt_seg, lens, skip):
-    """Per segment, the [start, end) arena bytes in_cksum_skip sums."""
-    n = pkt_seg.size - 1
-    seg_pkt = np.repeat(np.arange(n), np.diff(pkt_seg))
-    pos = np.cumsum(seg_len) - seg_len                      # global running position
-    pos = pos - (np.cumsum(seg_len) - seg_len)[pkt_seg[:-1]][seg_pkt]  # position in its chain
-    lo = np.clip(skip[seg_pkt] - pos, 0, seg_len)
-    hi = np.clip(lens[seg_pkt] - pos, 0, seg_len)
-    keep = hi > lo
-    return seg_off[keep] + lo[keep], seg_off[keep] + hi[keep], int((hi - lo)[keep].sum())
-
-
-def lines_touched(a, b, line):
-    first, last = a // line, (b - 1) // line
-    # union of [first, last] ranges over all segments
-    order = np.argsort(first, kind="stable")
-    f, l = first[order], last[order]
-    runmax = np.maximum.accumulate(l)
-    new = np.concatenate([[True], f[1:] > runmax[:-1]])
-    starts = f[new]
-    ends = np.maximum.reduceat(l, np.flatnonzero(new))
-    return int((ends - starts + 1).sum())
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="3", choices=["3", "3tx", "5tso"])
@@ -57,16 +33,18 @@ def main():
     else:
         lay = W.chain_layout(a.config, a.packets if a.config == "3tx" else None)
         lens, skip, seed = lay["lens"], lay["skip"], lay["seed"] is not None
-    s, e, algo = clipped_segments(lay["seg_off"], lay["seg_len"], lay["pkt_seg"], lens, skip)
     nseg, npkt = lay["seg_len"].size, lay["pkt_seg"].size - 1
-    desc_pkt = npkt * (4 + 4 + 4 + (4 if seed else 0)) + 4
-    res = {"config": a.config, "packets": npkt, "segments": nseg, "algorithmic_bytes": algo}
+    res = {"config": a.config, "packets": npkt, "segments": nseg}
     for line in (64, 128):
-        arena = lines_touched(s, e, line) * line
-        res[f"arena_lines_{line}B"] = arena
-        res[f"floor_wide_{line}B"] = arena + 12 * nseg + desc_pkt
-        res[f"floor_packed_{line}B"] = arena + 6 * nseg + desc_pkt
-        res[f"floor_wide_{line}B_over_algorithmic"] = round(res[f"floor_wide_{line}B"] / algo, 4)
+        wide = W.layout_floor(lay["seg_off"], lay["seg_len"], lay["pkt_seg"], lens, skip, seed, line)
+        packed = W.layout_floor(lay["seg_off"], lay["seg_len"], lay["pkt_seg"], lens, skip, seed,
+                                line, seg_desc_bytes=6)
+        algo = wide["algorithmic_bytes"]
+        res["algorithmic_bytes"] = algo
+        res[f"arena_lines_{line}B"] = wide["arena_bytes"]
+        res[f"floor_wide_{line}B"] = wide["floor_bytes"]
+        res[f"floor_packed_{line}B"] = packed["floor_bytes"]
+        res[f"floor_wide_{line}B_over_algorithmic"] = round(wide["floor_bytes"] / algo, 4)
     print(json.dumps(res))
 
 
