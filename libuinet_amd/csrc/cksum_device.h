@@ -180,6 +180,22 @@ struct Span {
     }
     return acc;
   }
+  // The first round (k0 = 0) of a packet: rounds u >= 1 are summed only when
+  // some lane of the wave holds a chunk there (loads past nch were skipped and
+  // left zero), so packets that fit G chunks -- aligned 64-B packets at 4
+  // lanes x 2 -- skip that vector work.
+  __device__ __forceinline__ uint32_t sum_lut_first(const MaskLut& lut, int gl) const {
+    uint32_t acc = lut.sum_oc(v[0], head - 16 * gl, end - 16 * gl);
+#pragma unroll
+    for (int u = 1; u < U; ++u) {
+      const uint32_t k = (uint32_t)(u * G + gl);
+      if (__ballot(k < nch)) {  // wave-uniform
+        const int b = 16 * (int)k;
+        acc += lut.sum_oc(v[u], head - b, end - b);
+      }
+    }
+    return acc;
+  }
   __device__ __forceinline__ uint64_t rest_lut(const MaskLut& lut, int gl) {
     uint64_t acc = 0;
     for (uint32_t k0 = G * U; k0 < nch; k0 += G * U) {

@@ -143,15 +143,16 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
       on = kStrided ? (uint64_t)pc * pkt_stride : off[pc];
       ln = kStrided ? fixed_len : len[pc];
     }
-    uint64_t acc;
+    uint32_t x;
     if (kLut) {
-      acc = l ? sp.sum_lut(lut, 0, gl) : 0;
-      if (sp.nch > (uint32_t)(G * U)) acc += sp.rest_lut(lut, gl);
+      // a span of one round folds its 32-bit sum (< U * 2^19) directly
+      const uint32_t a0 = l ? sp.sum_lut_first(lut, gl) : 0u;
+      x = sp.nch > (uint32_t)(G * U) ? fold16((uint64_t)a0 + sp.rest_lut(lut, gl)) : fold16_32(a0);
     } else {
-      acc = l ? sp.sum(0, gl) : 0;
+      uint64_t acc = l ? sp.sum(0, gl) : 0;
       if (sp.nch > (uint32_t)(G * U)) acc += sp.rest(gl);
+      x = fold16(acc);
     }
-    uint32_t x = fold16(acc);
     const uint32_t lp = parity ? parity[p] : 0u;
     if ((lp ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
     x = group_sum<G>(x);
