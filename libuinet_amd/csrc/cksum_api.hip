@@ -58,7 +58,7 @@ int check_launch() { return record_hip(hipGetLastError()); }
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_variant{0}, chains_pass{2}, host_threads{8},
       chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1}, walk_prefetch{1},
-      spans_contig{0}, spans_geo{0}, spans_sdesc{1}, spans_pipe{1};
+      spans_contig{0}, spans_geo{0}, spans_sdesc{1}, spans_pipe{1}, host_group{1};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -83,6 +83,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"spans_sdesc", &TuningLive::spans_sdesc, [](int v) { return v == 0 || v == 1; }},
       {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v >= 0 && v <= 2; }},
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
+      {"host_group", &TuningLive::host_group, [](int v) { return v >= 1 && v <= 64; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -101,7 +102,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_SPANS_LUT", "spans_lut"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
         {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_CONTIG", "spans_contig"},
         {"UINET_CKSUM_SPANS_GEO", "spans_geo"},         {"UINET_CKSUM_SPANS_SDESC", "spans_sdesc"},
-        {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},
+        {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},       {"UINET_CKSUM_HOST_GROUP", "host_group"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -135,6 +136,7 @@ Tuning tuning() {
   x.spans_geo = ld(t.spans_geo);
   x.spans_sdesc = ld(t.spans_sdesc);
   x.spans_pipe = ld(t.spans_pipe);
+  x.host_group = ld(t.host_group);
   return x;
 }
 
@@ -432,7 +434,8 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   const std::vector<Region>& regs = g_regions;
   const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const auto drain = [&]() { return record_hip(hipStreamSynchronize(c.stream)); };
-  const int group = std::max(1, threads);
+  // chunks per pipeline group: host_group per thread (one pool pass each)
+  const int group = std::max(1, threads) * std::max(1, tuning().host_group);
   size_t ring = 0;  // next free byte of the descriptor ring in c.h_buf
   uint64_t total = 0;
   size_t np_all = 0;

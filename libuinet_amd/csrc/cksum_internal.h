@@ -29,6 +29,8 @@ struct Tuning {
   int spans_geo;       // span kernels: lanes-per-packet G and loads-per-lane U
                        // as G * 16 + U (0 = picked from the mean length)
   int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead, 2 lockstep chase
+  int host_group;      // zero-copy host batches: chunks per thread in one pipeline
+                       // group (a pool pass walks a group while the GPU folds the last)
 };
 Tuning tuning();
 // True when G * 16 + U names a compiled span-kernel geometry.
