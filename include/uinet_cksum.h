@@ -168,12 +168,15 @@ int uinet_cksum_device_ok(void);
  *   "walk_prefetch"   host-mbuf batch walk: 0 = no prefetch, 1 = prefetch
  *                     mbuf headers a few packets ahead (default), 2 = chase
  *                     16 chains in lockstep (never changes results)
+ *   "host_group"      zero-copy host-mbuf batches: chunks per host thread in
+ *                     one pipeline group (1..64, default 1)
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
- * (0|1, or serial), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
+ * (0|1|2, or serial), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
  * UINET_CKSUM_CHAINS_TILE, UINET_CKSUM_XCD_REMAP, UINET_CKSUM_SPANS_LUT,
  * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF, UINET_CKSUM_SPANS_CONTIG,
- * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_SDESC and UINET_CKSUM_SPANS_PIPE set
+ * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_SDESC, UINET_CKSUM_SPANS_PIPE and
+ * UINET_CKSUM_HOST_GROUP set
  * the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
