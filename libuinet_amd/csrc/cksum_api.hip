@@ -58,7 +58,7 @@ int check_launch() { return record_hip(hipGetLastError()); }
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_variant{0}, chains_pass{2}, host_threads{8},
       chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1}, walk_prefetch{1},
-      spans_contig{0}, spans_geo{0}, spans_sdesc{1}, spans_pipe{1}, host_group{1};
+      spans_contig{0}, spans_geo{0}, spans_sdesc{1}, spans_pipe{1}, host_group{1}, host_pin{0};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -84,6 +84,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v >= 0 && v <= 2; }},
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
       {"host_group", &TuningLive::host_group, [](int v) { return v >= 1 && v <= 64; }},
+      {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -103,6 +104,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_CONTIG", "spans_contig"},
         {"UINET_CKSUM_SPANS_GEO", "spans_geo"},         {"UINET_CKSUM_SPANS_SDESC", "spans_sdesc"},
         {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},       {"UINET_CKSUM_HOST_GROUP", "host_group"},
+        {"UINET_CKSUM_HOST_PIN", "host_pin"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -137,6 +139,7 @@ Tuning tuning() {
   x.spans_sdesc = ld(t.spans_sdesc);
   x.spans_pipe = ld(t.spans_pipe);
   x.host_group = ld(t.host_group);
+  x.host_pin = ld(t.host_pin);
   return x;
 }
 
@@ -436,13 +439,14 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   const auto drain = [&]() { return record_hip(hipStreamSynchronize(c.stream)); };
   // chunks per pipeline group: host_group per thread (one pool pass each)
   const int group = std::max(1, threads) * std::max(1, tuning().host_group);
+  const bool pin = tuning().host_pin != 0;
   size_t ring = 0;  // next free byte of the descriptor ring in c.h_buf
   uint64_t total = 0;
   size_t np_all = 0;
   for (int g0 = 0; g0 < nch; g0 += group) {
     const int g1 = std::min(nch, g0 + group);
     clk::time_point ta = trace ? clk::now() : clk::time_point();
-    pool.run(g1 - g0, threads, [&](int jj) { walk_chunk(g0 + jj); });
+    pool.run(g1 - g0, threads, [&](int jj) { walk_chunk(g0 + jj); }, pin);
     clk::time_point tb = trace ? clk::now() : clk::time_point();
     if (trace) t_walk += std::chrono::duration<double, std::milli>(tb - ta).count();
 
@@ -500,7 +504,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
         ps[i - i0] = C.first_piece + B.pk_first[(size_t)i];
         sd[i - i0] = B.seed[(size_t)i];
       }
-    });
+    }, pin);
     ps[ng] = (uint32_t)np;
     for (int j = g0; j < g1; j++) bad |= B.chunks[(size_t)j].unmapped;
     if (trace) t_desc += std::chrono::duration<double, std::milli>(clk::now() - tb).count();
@@ -682,7 +686,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   }
 
   // (1) walk
-  pool.run(nch, threads, walk_chunk);
+  pool.run(nch, threads, walk_chunk, tuning().host_pin != 0);
 
   if (trace) t_walk = clk::now();
   // (2) place the chunks
@@ -737,7 +741,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
           }
           cur += ((uint64_t)B.bytes[(size_t)i] + 15) & ~uint64_t(15);
         }
-      });
+      }, tuning().host_pin != 0);
       if (stream_copy) {
         const uint64_t b0 = B.chunks[(size_t)g0].pack_base;
         const uint64_t b1 = g1 < nch ? B.chunks[(size_t)g1].pack_base : packed;

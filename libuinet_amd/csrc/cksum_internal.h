@@ -31,6 +31,7 @@ struct Tuning {
   int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead, 2 lockstep chase
   int host_group;      // zero-copy host batches: chunks per thread in one pipeline
                        // group (a pool pass walks a group while the GPU folds the last)
+  int host_pin;        // host pool helpers pinned to CPUs 1.. of the process mask (0/1)
 };
 Tuning tuning();
 // True when G * 16 + U names a compiled span-kernel geometry.

@@ -219,7 +219,8 @@ void for_chunks(int n, F&& f) {
   int cs = (n + threads * 4 - 1) / (threads * 4);
   if (cs < 1024) cs = 1024;
   const int nch = (n + cs - 1) / cs;
-  host_pool().run(nch, threads, [&](int j) { f(j * cs, j * cs + cs < n ? j * cs + cs : n); });
+  host_pool().run(nch, threads, [&](int j) { f(j * cs, j * cs + cs < n ? j * cs + cs : n); },
+                  tuning().host_pin != 0);
 }
 
 }  // namespace
