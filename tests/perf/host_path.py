@@ -58,8 +58,15 @@ def main():
             t1, r1 = R.time_skip(ch.heads, ln, sk, nthreads=1, reps=3)
             e["reference_1thread_gibs"] = round(gib / t1, 2)
             cpus = sorted(os.sched_getaffinity(0))[:16]
-            t16, r16 = R.time_skip(ch.heads, ln, sk, nthreads=len(cpus), cpus=cpus, reps=5)
+            # 16 threads pinned to the first CPUs of the mask, and floating:
+            # the faster is the baseline (profiles/r02/host_pin/)
+            t16p, r16 = R.time_skip(ch.heads, ln, sk, nthreads=len(cpus), cpus=cpus, reps=5)
+            t16f, r16f = R.time_skip(ch.heads, ln, sk, nthreads=len(cpus), cpus=None, reps=5)
+            t16 = min(t16p, t16f)
             e[f"reference_{len(cpus)}thread_gibs"] = round(gib / t16, 2)
+            e[f"reference_{len(cpus)}thread_pinned_gibs"] = round(gib / t16p, 2)
+            e[f"reference_{len(cpus)}thread_floating_gibs"] = round(gib / t16f, 2)
+            r16 = r16 if np.array_equal(r16, r16f) else r16f * 0  # both must match
             e["equal_reference"] = bool(np.array_equal(r1, r_zc) and np.array_equal(r16, r_zc))
         res[name] = e
         print(name, e, flush=True)
