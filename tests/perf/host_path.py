@@ -66,8 +66,8 @@ def main():
             e[f"reference_{len(cpus)}thread_gibs"] = round(gib / t16, 2)
             e[f"reference_{len(cpus)}thread_pinned_gibs"] = round(gib / t16p, 2)
             e[f"reference_{len(cpus)}thread_floating_gibs"] = round(gib / t16f, 2)
-            r16 = r16 if np.array_equal(r16, r16f) else r16f * 0  # both must match
-            e["equal_reference"] = bool(np.array_equal(r1, r_zc) and np.array_equal(r16, r_zc))
+            e["equal_reference"] = bool(np.array_equal(r1, r_zc) and np.array_equal(r16, r_zc)
+                                        and np.array_equal(r16f, r_zc))
         res[name] = e
         print(name, e, flush=True)
     print(json.dumps(res))
