@@ -216,6 +216,40 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def reference_results(cfg: str, w, threads: int):
+    """The reference's (or, without oracle/_ref, the oracle restatement's)
+    results over this rank's bytes, computed on the host after the timed
+    region: the distributed line's parity check (cpu_baseline leg)."""
+    import oracle
+    from libuinet_amd.mbuf import MbufChains
+
+    host = w["arena"].cpu().numpy()
+    R = oracle.Reference() if oracle.have_reference() else None
+    kind = "reference" if R is not None else "port"
+    threads = max(1, threads)
+    if cfg in CHAIN_CONFIGS:
+        lay = w["layout"]
+        ch = MbufChains(host, lay["seg_off"], lay["seg_len"], lay["pkt_seg"])
+        if cfg == "5tso":
+            args = (ch.heads, lay["plen"], 20, lay["src"], lay["dst"], 6)
+            out = R.time_pseudo(*args, nthreads=threads, reps=1)[1] if R else \
+                oracle.Oracle().pseudo_header_batch(*args)
+        else:
+            args = (ch.heads, lay["lens"], 20)
+            out = R.time_skip(*args, nthreads=threads, reps=1)[1] if R else \
+                oracle.Oracle().skip_batch(*args, nthreads=threads)
+    elif cfg == "5":
+        ch = MbufChains.contiguous(host, w["frame"] * np.arange(w["n"], dtype=np.int64), w["frame"])
+        args = (ch.heads, w["plen"], w["off0"], w["src"], w["dst"], w["proto"])
+        out = R.time_pseudo(*args, nthreads=threads, reps=1)[1] if R else \
+            oracle.Oracle().pseudo_header_batch(*args)
+    else:
+        ch = MbufChains.contiguous(host, w["off"].cpu().numpy(), w["length"])
+        out = R.time_skip(ch.heads, w["length"], 0, nthreads=threads, reps=1)[1] if R else \
+            oracle.Oracle().skip_batch(ch.heads, w["length"], 0, nthreads=threads)
+    return kind, np.ascontiguousarray(out, dtype=np.uint16)
+
+
 def cpu_baseline(cfg: str, w, gpu_out, threads: int):
     """The reference's scalar in_cksum_skip / in_cksum_pseudo_header over the same
     bytes as host mbufs; returns the cpu_baseline object (and checks parity)."""
@@ -255,40 +289,46 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
         timer = (lambda nt, cp, r: R.time_skip(*args, nthreads=nt, cpus=cp, reps=r)) if R else None
         port = lambda: oracle.Oracle().skip_batch(*args, nthreads=threads)  # noqa: E731
     gib = w["bytes"] / 2**30
-    placement = "pinned"
+    runs = {}
     if timer is not None:
-        t1, out1 = timer(1, cpus[:1], 3)
-        # median of 5 single passes each way (one best-of-5 on a shared box once
-        # read an impossible 1.7 TB/s, profiles/r02/final/NOTES.md), the threads
-        # pinned to the first CPUs of the mask and left to the scheduler: on a
-        # 256-CPU box the floating threads spread over more caches and memory
-        # channels and ran 1.3-2x faster (profiles/r02/host_pin/); the faster is
-        # the baseline
-        pin_runs, float_runs = [], []
-        for _ in range(5):
-            pin_runs.append(timer(threads, cpus, 1))
-            float_runs.append(timer(threads, None, 1))
-        t_pin = float(np.median([r[0] for r in pin_runs]))
-        t_float = float(np.median([r[0] for r in float_runs]))
-        tn, outn = (t_pin, pin_runs[-1][1]) if t_pin <= t_float else (t_float, float_runs[-1][1])
-        placement = "pinned" if t_pin <= t_float else "floating"
-        out_other = float_runs[-1][1] if placement == "pinned" else pin_runs[-1][1]
+        # median of 5 single passes per (threads, placement): the threads pinned
+        # to the first CPUs of the process mask, and left to the scheduler (on
+        # the GPU box's 256-CPU mask floating threads spread over more caches
+        # and memory channels and ran 1.3-2x faster, profiles/r02/host_pin/).
+        # One best-of-5 on a shared box once read an impossible 1.7 TB/s
+        # (profiles/r02/final/NOTES.md), hence medians.  `threads` is the box's
+        # CPU share (16 per GPU): the rest of the mask belongs to the other
+        # GPUs' jobs on the machine.
+        outs = []
+        for nt in sorted({1, threads}):
+            for placement in ("pinned", "floating"):
+                rr = [timer(nt, cpus[:nt] if placement == "pinned" else None, 1)
+                      for _ in range(5)]
+                runs[f"{nt}_{placement}"] = float(np.median([r[0] for r in rr]))
+                outs.append(rr[-1][1])
+        best = min((k for k in runs if k.startswith(f"{threads}_")), key=runs.get)
+        tn = runs[best]
+        t1 = min(runs["1_pinned"], runs["1_floating"])
     else:  # oracle restatement, timed the same way
-        t0 = time.perf_counter(); out1 = port(); t1 = time.perf_counter() - t0  # noqa: E702
-        tn, outn, out_other = t1, out1, out1
-        t_pin = t_float = t1
-    parity = bool(np.array_equal(outn, gpu_out) and np.array_equal(out1, gpu_out)
-                  and np.array_equal(out_other, gpu_out))
+        t0 = time.perf_counter(); o = port(); t1 = time.perf_counter() - t0  # noqa: E702
+        outs, tn, best = [o], t1, f"{threads}_port"
+        runs[best] = t1
+    parity = bool(all(np.array_equal(o, gpu_out) for o in outs))
+    rates = {k: round(gib / t, 3) for k, t in runs.items()}
     return {
         "value": round(gib / tn, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
         "cpu_model": cpu_model(),
         "sample": (f"{w['n']:,} packets ({gib:.3f} GiB algorithmic) of the benchmarked batch, "
-                   f"host copy as {'chained ' if cfg in CHAIN_CONFIGS else ''}struct mbuf; median of 5 on "
-                   f"{threads} threads, the faster of pinned ({gib / t_pin:.3f} GiB/s) and "
-                   f"floating ({gib / t_float:.3f} GiB/s); 1 thread: {gib / t1:.3f} GiB/s best of "
-                   f"3; results bit-identical to the GPU: {parity}"),
-        "placement": placement,
+                   f"host copy as {'chained ' if cfg in CHAIN_CONFIGS else ''}struct mbuf; median "
+                   f"of 5 passes per thread count and placement (GiB/s: "
+                   + ", ".join(f"{k.replace('_', ' threads ')} {v}" for k, v in rates.items())
+                   + f"); value = {best.replace('_', ' threads ')}; results bit-identical to "
+                   f"the GPU in every run: {parity}"),
+        "runs_gibs": rates,
+        "value_from": best,
+        "placement": best.split("_")[1],
         "one_thread_gibs": round(gib / t1, 3),
+        "mask_cpus": len(allowed),
         "bit_identical_to_gpu": parity,
     }
 
@@ -351,13 +391,16 @@ def main():
     outs = [torch.empty(n, dtype=torch.uint16, device="cuda") for _ in range(NBUF)]
     out = outs[0]
     stream = torch.cuda.current_stream()
-    if distributed and backend == "nccl":
+    if distributed:
         # a non-blocking stream of its own for the kernels (made current, so
-        # the collectives order themselves after it) instead of the null
-        # stream: 0.481 vs 0.489 ms per step at world 1 (profiles/r02/gather/).
-        # High priority: a hardware queue apart from RCCL's normal-priority
-        # stream, so that step k's gather kernel does not sit between the
-        # kernels of steps k + 1 and k + 2
+        # the collectives and gloo's host copies order themselves after it)
+        # instead of the null stream: 0.481 vs 0.489 ms per step at world 1
+        # (profiles/r02/gather/).  High priority: a hardware queue apart from
+        # RCCL's normal-priority stream, so that step k's gather kernel does
+        # not sit between the kernels of steps k + 1 and k + 2.  Both backends
+        # run this same layout (round 2's gloo rehearsal kept the null stream
+        # after a side-stream run exited non-zero before the ordering below
+        # existed; profiles/r03/gather/)
         stream = torch.cuda.Stream(priority=-1)
         # it does not synchronise with the null stream: the workload's
         # generation and descriptor uploads (null stream) must be complete
@@ -485,6 +528,29 @@ def main():
         torch.cuda.synchronize()
         gpu_out = outs[(K - 1) % NBUF].cpu().view(torch.int16).numpy().view(np.uint16)
         result["cpu_baseline"] = cpu_baseline(args.config, w, gpu_out, args.cpu_threads)
+        result["bit_identical"] = result["cpu_baseline"]["bit_identical_to_gpu"]
+        result["parity"] = {"packets": n, "against": result["cpu_baseline"]["kind"],
+                            "how": "the last timed step's results vs the reference's "
+                                   "in_cksum_* over the same bytes as host mbufs"}
+    elif distributed and args.cpu_baseline == "auto":
+        # every rank folds its own bytes with the reference on its host cores
+        # (after the timed region), the expected results meet on rank 0 in
+        # one more gather, and rank 0 compares them with the gathered GPU
+        # results of the last timed step: the N > 1 line proves its own parity
+        torch.cuda.synchronize()
+        kind, want = reference_results(args.config, w, args.cpu_threads)
+        from libuinet_amd.dist import gather_results
+
+        allwant = gather_results(torch.from_numpy(want.view(np.int16)).to(
+            "cuda" if backend == "nccl" else "cpu"), counts)
+        if rank == 0:
+            got = rg.result((K - 1) % NBUF).cpu().numpy().view(np.uint16)
+            exp = allwant.cpu().numpy().view(np.uint16)
+            result["bit_identical"] = bool(got.shape == exp.shape and np.array_equal(got, exp))
+            result["parity"] = {"packets": int(exp.size), "against": kind,
+                                "how": "the last timed step's gathered results vs the "
+                                       "reference's in_cksum_* over every rank's bytes as host "
+                                       "mbufs, computed on each rank's host cores and gathered"}
     if args.save_results and rank == 0:
         last = (K - 1) % NBUF
         res = rg.result(last) if rg is not None else outs[last].view(torch.int16)

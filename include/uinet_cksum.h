@@ -92,9 +92,13 @@ uinet_in_cksum_update(void *ip_hdr)
 
 /* The reference's own name and type (in_cksum.h:46-61: defined when
  * <netinet/ip.h> has set IPVERSION 4), for code that includes this header
- * instead of <machine/in_cksum.h>; a translation unit that includes the
- * reference header keeps the reference's definition. */
-#if defined(IPVERSION) && (IPVERSION == 4) && !defined(_MACHINE_IN_CKSUM_H_)
+ * instead of <machine/in_cksum.h>.  Include order: a translation unit that
+ * also includes the reference header must include it FIRST (its guard
+ * _MACHINE_IN_CKSUM_H_ then hides this copy), or define
+ * UINET_CKSUM_NO_IN_CKSUM_UPDATE before including this header; otherwise
+ * the two inline definitions collide. */
+#if defined(IPVERSION) && (IPVERSION == 4) && !defined(_MACHINE_IN_CKSUM_H_) && \
+    !defined(UINET_CKSUM_NO_IN_CKSUM_UPDATE)
 static inline void
 in_cksum_update(struct ip *ip)
 {

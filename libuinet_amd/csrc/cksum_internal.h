@@ -47,6 +47,12 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
                  uint32_t flags, uint32_t len_hint, hipStream_t stream);
 int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const uint32_t* seed,
                    uint16_t* out, uint32_t n, uint32_t flags, hipStream_t stream);
+// k_spans_lean (cksum_spans.hip): G = 32 or 64 lanes per packet; strided
+// takes packet i at base + i * stride, slen bytes (off / len unused).
+int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len,
+                      const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                      uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
+                      int blocks_cu, hipStream_t stream);
 int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
                   const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                   const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,

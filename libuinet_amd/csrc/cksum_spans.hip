@@ -1,0 +1,466 @@
+// k_spans_lean: the span kernel for 32 and 64 lanes per packet (packets of
+// 0.7 KB and up; config 2's 1500 B, config 4, config 5's 9000 B).
+//
+// Same arithmetic as the other span kernels (cksum_device.h; reference
+// /root/reference/sys/amd64/amd64/in_cksum.c:91-170,193-232): every byte at
+// logical position p adds byte * 256^(p&1), folded with end-around carry.
+//
+// What it changes is the vector work per byte.  A streaming read that also
+// issues ~64 vector instructions per 16-B chunk and lane makes the platform
+// throttle 10-20 launches into a burst, one with ~32 does not
+// (profiles/r02/cold_ab/ section 4); k_spans_pp issued ~42 per KiB, most of
+// them per packet, not per byte.  Here every per-packet quantity is
+// wave-uniform scalar work and the per-packet vector work is shared:
+//
+//  * Descriptors.  A wave folds kP = 64 / G packets per step (one per lane
+//    group).  Their offsets, lengths, seeds and parity bytes come in by
+//    scalar loads, and the scalar unit derives each packet's first aligned
+//    chunk, head, end, last chunk, rotation and folded seed.  A lane takes its
+//    group's value with one AND and one add (no v_cndmask pairs).
+//  * Loads.  The wave's packets are addressed from one scalar base (the
+//    lowest first chunk) plus a 32-bit lane offset: `global_load_dwordx4 v,
+//    voff, s[base]`, one v_min per slot for the clamp to the last chunk.  A
+//    wave whose packets lie 4 GiB apart takes per-lane 64-bit addresses.
+//  * Masks.  One ds_read_b128 from the 17 x 17 LDS table per chunk slot; a
+//    slot that every packet of the wave covers whole (slot 1 of a 1500-B
+//    packet) skips the table and the ANDs.  The table is copied from a
+//    constant image in global memory instead of being computed per block.
+//  * Sums.  Each chunk is 4 v_dot2_u32_u16 against (1, 1) into a 32-bit
+//    lane partial (< 2^21, no fold before the reduction).
+//  * Reduction, two steps at once.  A group's partials of packet A (step k)
+//    and packet B (step k + 1) meet in one v_permlane16_swap (G = 32) or
+//    v_permlane32_swap + v_permlane16_swap (G = 64), then 4 DPP row_ror adds:
+//    each 16-lane row then holds one packet's total, and the fold, the
+//    rotation (a shift by 0 or 8 and one more fold), the seed, the complement
+//    and the store run once for 2 (G = 64) or 4 (G = 32) packets.
+//  * Pipelining as in k_spans_pp: step k + 1's chunks are loaded before step
+//    k is summed, every load unconditional, so the wait for step k leaves step
+//    k + 1's loads in flight.  Spans longer than one round (16 G U bytes)
+//    finish with serial rounds.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "cksum_device.h"
+
+namespace uinet {
+namespace {
+
+constexpr int kU = 3;  // chunk loads per lane and packet in one round
+
+// The 17 x 17 chunk-mask table (entry s * 17 + e keeps bytes [s, e) of a
+// 16-byte chunk) as a constant image: a block copies it into LDS with one
+// 16-byte load per thread instead of computing it (~30 VALU per entry).
+struct alignas(16) MaskWords {
+  uint32_t w[17 * 17 * 4];
+};
+constexpr MaskWords make_mask_words() {
+  MaskWords t{};
+  for (int s = 0; s < 17; ++s)
+    for (int e = 0; e < 17; ++e)
+      for (int d = 0; d < 4; ++d) {
+        uint32_t m = 0;
+        for (int b = 0; b < 4; ++b)
+          if (4 * d + b >= s && 4 * d + b < e) m |= 0xffu << (8 * b);
+        t.w[(s * 17 + e) * 4 + d] = m;
+      }
+  return t;
+}
+__device__ const MaskWords g_mask_words = make_mask_words();
+
+__device__ __forceinline__ void lut_copy(MaskLut& lut) {
+  const u32x4* src = reinterpret_cast<const u32x4*>(g_mask_words.w);
+  for (int i = threadIdx.x; i < 17 * 17; i += blockDim.x) lut.m[i] = src[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// A wave-uniform value the compiler may not reason about (keeps 32-bit
+// compares of a 64-bit value's halves from being merged back into a 64-bit
+// compare, which only the vector ALU has).
+__device__ __forceinline__ uint32_t opaque_s(uint32_t x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
+// Scalar (SMEM) loads: through the constant address space a uniform load of
+// memory the kernel never writes becomes an s_load.
+__device__ __forceinline__ uint64_t sld64(const uint64_t* p) {
+  const uint64_t v = *(const __attribute__((address_space(4))) uint64_t*)(uintptr_t)p;
+  return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
+}
+__device__ __forceinline__ uint32_t sld32(const uint32_t* p) {
+  return rfl(*(const __attribute__((address_space(4))) uint32_t*)(uintptr_t)p);
+}
+// The byte at p, from the aligned dword that holds it (never crosses a page).
+__device__ __forceinline__ uint32_t sld8(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return (sld32(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)) >> (8 * (a & 3))) & 0xffu;
+}
+
+// Four dot2 against (1, 1): both 16-bit halves of every word added into acc.
+__device__ __forceinline__ uint32_t dot_acc(u32x4 v, uint32_t acc) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  const us2 one = {1, 1};
+  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, (uint32_t)v.x), one, acc, false);
+  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, (uint32_t)v.y), one, acc, false);
+  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, (uint32_t)v.z), one, acc, false);
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, (uint32_t)v.w), one, acc, false);
+}
+__device__ __forceinline__ uint32_t dot_acc_masked(u32x4 v, u32x4 m, uint32_t acc) {
+  return dot_acc(v & m, acc);
+}
+
+// x + the value of row_ror:n (lanes rotate by n inside each 16-lane row).
+template <int kN>
+__device__ __forceinline__ uint32_t add_ror(uint32_t x) {
+  return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x120 + kN, 0xf, 0xf, false);
+}
+
+// One step of a wave: the descriptors of its kP packets (one per lane group),
+// in SGPRs.  o / l are the span offset from `base` and its length (an empty
+// span borrows its neighbour's offset, or 0, so that its re-read chunk is
+// one the wave reads anyway); rot holds the packets' rotation bits
+// (address parity != logical parity, in_cksum.c:222-225) already placed at
+// the reduction rows of an A step (G = 32: rows 0 / 2; G = 64: rows 0, 1);
+// sd the folded seeds (the in_cksum_pseudo_header sum, in_cksum.c:241-276).
+template <int kP>
+struct Step {
+  uint64_t o[kP];
+  uint32_t l[kP];
+  uint32_t rot;
+  uint32_t sd[kP];
+};
+// What a step's sum needs from its load: head (span start inside its first
+// chunk) and end (head + len) per packet, and whether the pair lies too far
+// apart for 32-bit lane offsets from one scalar base.
+template <int kP>
+struct Geo {
+  uint32_t h[kP], e[kP];
+  bool far;
+};
+
+template <int G, bool kParity, bool kSeed, bool kStrided>
+__global__ __launch_bounds__(kBlock) void k_spans_lean(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed,
+    const uint8_t* __restrict__ parity, uint16_t* __restrict__ out, uint32_t n, uint32_t flags,
+    uint32_t remap, uint64_t stride, uint32_t slen) {
+  static_assert(G == 32 || G == 64, "one or two packets per wave");
+  constexpr int kP = 64 / G;
+  constexpr uint32_t kGroups = kBlock / G;
+  constexpr uint32_t kRound = 16u * G * kU;  // bytes of a span one round covers
+  constexpr uint32_t kBias = 0x80000000u;    // lane offsets are biased: pairs may lie either way
+  __shared__ MaskLut lut;
+  // the table entry at byte address a (= 16 x entry index)
+  auto lut_at = [&](uint32_t a) -> u32x4 {
+    return *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(lut.m) + a);
+  };
+
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t gl = lane & (G - 1);
+  const uint32_t pos0 = 16u * gl;             // byte of this lane's slot-0 chunk in its span
+  const uint32_t negpos16 = 0u - 16u * pos0;  // the same in mask-table units, negated
+  const uint32_t m0 = gl == 0 ? ~0u : 0u;     // the lane that holds a span's head chunk
+  // ~0 in the lanes of group 1 (kP = 2): a lane's value of a per-packet
+  // quantity is a0 + ((a1 - a0) & gmask).  Opaque, so that the compiler keeps
+  // one AND and one add instead of a v_mov / v_mov / v_cndmask select.
+  uint32_t gmask = (kP == 2 && lane >= 32) ? ~0u : 0u;
+  asm volatile("" : "+v"(gmask));
+  auto gsel = [&](const uint32_t (&a)[kP]) -> uint32_t {
+    if constexpr (kP == 1) return a[0];
+    else return a[0] + ((a[1] - a[0]) & gmask);
+  };
+
+  const uint32_t boff = (uint32_t)(reinterpret_cast<uintptr_t>(base) & 15);
+  const uint8_t* base_m = base - kBias;  // a step's loads: base_m + o[0] + (biased) lane offset
+  // packets per grid step; the host keeps n + 3 S below 2^32
+  const uint32_t S = gridDim.x * kGroups;
+  const uint32_t wave = rfl(threadIdx.x) / 64;
+  uint32_t q = logical_block(remap) * kGroups + wave * kP;  // the wave's first packet (even)
+
+  // Per 16-lane row r after the reduction: which packet of the pair, as an
+  // offset from the step's first packet.  G = 32: rows are (A g0, B g0, A g1,
+  // B g1); G = 64: (A, A, B, B).
+  const uint32_t row = lane >> 4;
+  const uint32_t row_b = kP == 2 ? (row & 1) : (row >> 1);  // 1 = packet B (step k + 1)
+  const uint32_t row_g = kP == 2 ? (row >> 1) : 0;          // lane group
+  const uint32_t row_sh8 = 8 * row;                         // this row's byte in rr
+  const uint32_t row_q = row_g + (row_b ? S : 0u);          // its packet - the step's first
+  const bool store_lane = kP == 2 ? (lane & 15) == 0 : (lane & 31) == 0;
+  // the results as a buffer resource of 2 n bytes (n < 2^31)
+  const __amdgpu_buffer_rsrc_t out_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(2u * n), 0x00020000);
+
+  // Descriptors of the step at q0 (< n; q0 even when kP = 2, so a pair's
+  // offsets and lengths are adjacent words).
+  auto desc = [&](uint32_t q0) {
+    Step<kP> s;
+    const bool two = kP == 2 && q0 + 1 < n;
+    if constexpr (kStrided) {
+      s.o[0] = (uint64_t)q0 * stride;
+      s.l[0] = slen;
+      if constexpr (kP == 2) {
+        s.o[1] = s.o[0] + stride;
+        s.l[1] = two ? slen : 0u;
+      }
+    } else {
+      s.o[0] = sld64(off + q0);
+      s.l[0] = sld32(len + q0);
+      if constexpr (kP == 2) {
+        s.o[1] = two ? sld64(off + q0 + 1) : s.o[0];
+        s.l[1] = two ? sld32(len + q0 + 1) : 0u;
+      }
+    }
+    uint32_t b[kP];
+#pragma unroll
+    for (int g = 0; g < kP; ++g) {
+      const uint32_t lp = kParity ? (g == 0 || two ? sld8(parity + q0 + g) : 0u) : 0u;
+      b[g] = (lp ^ boff ^ (uint32_t)s.o[g]) & 1u;
+      s.sd[g] = kSeed ? (g == 0 || two ? fold16_32(sld32(seed + q0 + g)) : 0u) : 0u;
+    }
+    if constexpr (kP == 2) {
+      s.rot = b[0] | (b[1] << 2);
+      if (!s.l[0]) s.o[0] = s.l[1] ? s.o[1] : 0;
+      if (!s.l[1]) s.o[1] = s.o[0];
+    } else {
+      s.rot = b[0] * 3u;
+      if (!s.l[0]) s.o[0] = 0;
+    }
+    return s;
+  };
+
+  // Where a step's chunks are: one scalar base for the wave, and per packet
+  // its first chunk d and last chunk lo as biased 32-bit offsets from it.  A
+  // far pair (offsets 1 GiB or more apart, or a span of 1 GiB or more) loads
+  // packet 0's chunks in both groups; far_sum folds it again.
+  struct Addr {
+    const uint8_t* sb;
+    uint32_t d[kP], lo[kP];
+  };
+  auto addr = [&](const Step<kP>& s, Geo<kP>& z) {
+    Addr w;
+    uint32_t lastb[kP];
+#pragma unroll
+    for (int g = 0; g < kP; ++g) {
+      z.h[g] = ((uint32_t)s.o[g] + boff) & 15u;
+      z.e[g] = z.h[g] + s.l[g];
+      lastb[g] = (max(z.e[g], 1u) - 1u) & ~15u;  // 16 x the last chunk (0 when empty)
+      w.d[g] = kBias - z.h[g];
+    }
+    w.sb = base_m + s.o[0];
+    z.far = false;
+    if constexpr (kP == 2) {
+      const uint64_t df = s.o[1] - s.o[0];
+      const uint32_t dlo = (uint32_t)df, dhi = opaque_s((uint32_t)(df >> 32));
+      z.far = dhi != (uint32_t)((int32_t)dlo >> 31) || dlo + 0x40000000u >= kBias ||
+              (lastb[0] | lastb[1]) >= 0x40000000u;
+      w.d[1] += dlo;
+      if (z.far) {
+        w.d[1] = w.d[0];
+        lastb[1] = lastb[0];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < kP; ++g) w.lo[g] = w.d[g] + lastb[g];
+    return w;
+  };
+  // Chunk slot u of round r (byte rb = r * kRound of the span): lane offsets
+  // pos0 + rb + 16 u G from the packet's first chunk, clamped to its last.
+  auto load_round = [&](const Addr& w, uint32_t rb, u32x4 (&v)[kU]) {
+    const uint32_t b = gsel(w.d) + pos0 + rb, l = gsel(w.lo);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) v[u] = load_chunk(w.sb + min(b + 16u * u * G, l));
+  };
+  auto load_step = [&](const Step<kP>& s, u32x4 (&v)[kU]) {
+    Geo<kP> z;
+    load_round(addr(s, z), 0, v);
+    return z;
+  };
+
+  // A far step's lane partial, every round with per-lane 64-bit addresses.
+  auto far_sum = [&](const Step<kP>& s, const Geo<kP>& z) -> uint32_t {
+    uint32_t chi[kP], clo[kP], lb[kP], emax = 0;
+#pragma unroll
+    for (int g = 0; g < kP; ++g) {
+      const uint64_t c0 = s.o[g] - z.h[g];
+      chi[g] = (uint32_t)(c0 >> 32);
+      clo[g] = (uint32_t)c0;
+      lb[g] = (max(z.e[g], 1u) - 1u) & ~15u;
+      emax = max(emax, z.e[g]);
+    }
+    const uint8_t* pb = base + (((uint64_t)gsel(chi) << 32) | gsel(clo));
+    const uint32_t l = gsel(lb), e0 = gsel(z.e) - pos0, h0 = gsel(z.h) - pos0;
+    uint32_t acc = 0;
+    for (uint32_t rb = 0; rb < emax; rb += kRound) {  // wave-uniform
+      u32x4 w[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) w[u] = load_chunk(pb + min(pos0 + rb + 16u * u * G, l));
+      uint32_t r = 0;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const uint32_t k = rb + 16u * u * G;
+        r = dot_acc_masked(w[u], lut.m[MaskLut::index((int)(h0 - k), (int)(e0 - k))], r);
+      }
+      acc = fold16_32(acc) + r;
+    }
+    return acc;
+  };
+
+  // The lane partial of one step: round 0 from registers, later rounds
+  // (spans longer than kRound) serially.  Mask-table addresses are 16 x the
+  // entry index: 272 x head + 16 x clamp(end - chunk start, 0, 16).
+  auto sum_step = [&](const Step<kP>& s, const Geo<kP>& z, const u32x4 (&v)[kU]) -> uint32_t {
+    if (z.far) return far_sum(s, z);  // wave-uniform, rare
+    uint32_t E[kP], H[kP], emin = z.e[0], emax = z.e[0];
+#pragma unroll
+    for (int g = 0; g < kP; ++g) {
+      E[g] = 16u * min(z.e[g], 1u << 20);  // round 0 cannot tell 2^20 from more
+      H[g] = 272u * z.h[g];
+      emin = min(emin, z.e[g]);
+      emax = max(emax, z.e[g]);
+    }
+    const uint32_t e16 = gsel(E) + negpos16;
+    uint32_t acc = dot_acc_masked(v[0], lut_at((gsel(H) & m0) + clampi((int)e16, 0, 256)), 0u);
+#pragma unroll
+    for (int u = 1; u < kU; ++u) {
+      if (emin >= 16u * (u + 1) * G)  // wave-uniform: every lane's chunk is whole
+        acc = dot_acc(v[u], acc);
+      else
+        acc = dot_acc_masked(v[u], lut_at(clampi((int)(e16 - 256u * u * G), 0, 256)), acc);
+    }
+    if (emax > kRound) {  // wave-uniform
+      Geo<kP> z2;
+      const Addr w = addr(s, z2);
+      const uint32_t e0 = gsel(z.e) - pos0;
+      for (uint32_t rb = kRound; rb < emax; rb += kRound) {
+        u32x4 x[kU];
+        load_round(w, rb, x);
+        uint32_t r = 0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          r = dot_acc_masked(x[u], lut.m[clampi((int)(e0 - rb - 16u * u * G), 0, 16)], r);
+        acc = fold16_32(acc) + r;  // < 2^21: 64 lanes of it still fit 32 bits
+      }
+    }
+    return acc;
+  };
+
+  // Packets A (step at q0) and B (step at q0 + S): reduce, fold, rotate, seed,
+  // complement and store, once for the 2 * kP packets.
+  auto finish = [&](uint32_t xA, uint32_t xB, const Step<kP>& sA, const Step<kP>& sB,
+                    uint32_t q0) {
+    uint32_t t;
+    if constexpr (kP == 2) {
+      const auto r = __builtin_amdgcn_permlane16_swap(xA, xB, false, false);
+      t = r[0] + r[1];  // rows: A g0, B g0, A g1, B g1 (16-lane partials)
+    } else {
+      const auto r = __builtin_amdgcn_permlane32_swap(xA, xB, false, false);
+      const uint32_t h = r[0] + r[1];  // lanes 0-31: A, 32-63: B
+      const auto r2 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+      t = r2[0] + r2[1];  // rows: A, A, B, B
+    }
+    t = add_ror<8>(t);
+    t = add_ror<4>(t);
+    t = add_ror<2>(t);
+    t = add_ror<1>(t);  // every lane: its row's total (< 2^27)
+    // row r rotates by 8 when bit r of rowrot is set: rr = 8 in byte r
+    const uint32_t rowrot = sA.rot | (sB.rot << (kP == 2 ? 1 : 2));
+    const uint32_t rr = ((rowrot * 0x00204081u) & 0x01010101u) << 3;
+    uint32_t x = fold16_32(t);
+    x = fold16_32(x << __builtin_amdgcn_ubfe(rr, row_sh8, 8));  // x * 256^rot mod 65535
+    if constexpr (kSeed) {
+      if constexpr (kP == 2) {
+        const uint32_t ss0 = sA.sd[0] | (sB.sd[0] << 16);  // rows 0, 1
+        const uint32_t ss1 = sA.sd[1] | (sB.sd[1] << 16);  // rows 2, 3
+        x = fold16_32(x + __builtin_amdgcn_ubfe(row_g ? ss1 : ss0, 16 * row_b, 16));
+      } else {
+        x = fold16_32(x + __builtin_amdgcn_ubfe(sA.sd[0] | (sB.sd[0] << 16), 16 * row_b, 16));
+      }
+    }
+    uint32_t res = x;
+    if (!(flags & UINET_CKSUM_F_NO_COMPLEMENT)) {
+      res = ~x & 0xffffu;
+      if ((flags & UINET_CKSUM_F_UDP) && res == 0) res = 0xffff;  // ip_output.c:962-963
+    }
+    // no branch around the store (a divergent branch here made the whole
+    // loop's descriptors divergent): lanes that do not store address past
+    // the end of the buffer resource, and the hardware drops the write
+    const uint32_t qr = q0 + row_q;
+    const uint32_t ob = store_lane && qr < n ? 2u * qr : 0xfffffff0u;
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, out_rsrc, (int)ob, 0, 0);
+  };
+
+  // Steps run two at a time, A and B; the next A's chunks are loaded while B
+  // is summed.  A wave loads no step past the end of the batch: its last one
+  // or two steps leave the loop by their own branch.  Descriptors are fetched
+  // two steps ahead (clamped to the batch: a clamped fetch is never loaded).
+  u32x4 vA[kU], vB[kU];
+  Step<kP> sA = desc(min(q, (n - 1) & ~(uint32_t)(kP - 1)));
+  Geo<kP> zA = load_step(sA, vA);  // the first step's bytes are in flight ...
+  lut_copy(lut);  // ... while the block copies its mask table (every thread
+                  // reaches this barrier: no exit before it)
+  if (q >= n) return;  // wave-uniform
+  const uint32_t qmax = (n - 1) & ~(uint32_t)(kP - 1);  // the last step start
+  Step<kP> sB = desc(min(q + S, qmax));
+  for (;;) {
+    if (q + S >= n) {
+      finish(sum_step(sA, zA, vA), 0u, sA, sA, q);
+      break;
+    }
+    const Geo<kP> zB = load_step(sB, vB);  // step q + S in flight while step q is summed
+    const Step<kP> sC = desc(min(q + 2 * S, qmax));
+    const uint32_t xA = sum_step(sA, zA, vA);
+    if (q + 2 * S >= n) {
+      finish(xA, sum_step(sB, zB, vB), sA, sB, q);
+      break;
+    }
+    zA = load_step(sC, vA);  // step q + 2S in flight while step q + S is summed
+    const Step<kP> sD = desc(min(q + 3 * S, qmax));
+    finish(xA, sum_step(sB, zB, vB), sA, sB, q);
+    q += 2 * S;
+    sA = sC;
+    sB = sD;
+  }
+}
+
+}  // namespace
+
+int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len,
+                      const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                      uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
+                      int blocks_cu, hipStream_t stream) {
+  const uint32_t groups = kBlock / g;
+  uint64_t blocks = ((uint64_t)n + groups - 1) / groups;
+  // the kernel's 32-bit packet indices need n + 3 * blocks * groups < 2^32
+  const uint64_t cap = std::min<uint64_t>(256ull * (uint64_t)blocks_cu, (1ull << 26) / groups);
+  blocks = std::max<uint64_t>(1, std::min(blocks, cap));
+  const dim3 grid((uint32_t)blocks), blk(kBlock);
+  const uint8_t* b = static_cast<const uint8_t*>(base);
+  const uint32_t remap = (uint32_t)tuning().xcd_remap;
+#define UINET_LEAN(G, P, SD, ST)                                                              \
+  hipLaunchKernelGGL((k_spans_lean<G, P, SD, ST>), grid, blk, 0, stream, b, off, len, seed, \
+                     parity, out, n, flags, remap, stride, slen)
+#define UINET_LEAN_G(G)                                          \
+  if (strided) {                                                 \
+    if (seed) UINET_LEAN(G, false, true, true);                  \
+    else UINET_LEAN(G, false, false, true);                      \
+  } else if (parity) {                                           \
+    if (seed) UINET_LEAN(G, true, true, false);                  \
+    else UINET_LEAN(G, true, false, false);                      \
+  } else {                                                       \
+    if (seed) UINET_LEAN(G, false, true, false);                 \
+    else UINET_LEAN(G, false, false, false);                     \
+  }
+  if (g == 32) {
+    UINET_LEAN_G(32)
+  } else {
+    UINET_LEAN_G(64)
+  }
+#undef UINET_LEAN_G
+#undef UINET_LEAN
+  return check_launch();
+}
+
+}  // namespace uinet

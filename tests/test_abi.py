@@ -107,6 +107,29 @@ def test_in_cksum_update_inline(tmp_path):
         assert _ip_fold(bytes(buf)) == 0xFFFF
 
 
+@pytest.mark.parametrize("order", ["reference_first", "opt_out_macro", "ours_only"])
+def test_in_cksum_update_include_order(tmp_path, order):
+    """The reference-named in_cksum_update shim next to a reference-style
+    definition (in_cksum.h:46-61 under its _MACHINE_IN_CKSUM_H_ guard): with
+    the reference header first, or with UINET_CKSUM_NO_IN_CKSUM_UPDATE, the
+    unit compiles with one definition; alone, the shim provides it."""
+    ref_like = ("#ifndef _MACHINE_IN_CKSUM_H_\n#define _MACHINE_IN_CKSUM_H_\n"
+                "static inline void in_cksum_update(struct ip *ip) { (void)ip; }\n#endif\n")
+    head = "#define IPVERSION 4\nstruct ip;\n"
+    if order == "reference_first":
+        body = head + ref_like + '#include "uinet_cksum.h"\n'
+    elif order == "opt_out_macro":
+        body = head + '#define UINET_CKSUM_NO_IN_CKSUM_UPDATE\n#include "uinet_cksum.h"\n' + \
+            ref_like.replace("#ifndef _MACHINE_IN_CKSUM_H_\n#define _MACHINE_IN_CKSUM_H_\n", "") \
+            .replace("#endif\n", "")
+    else:
+        body = head + '#include "uinet_cksum.h"\n'
+    src = tmp_path / "order.c"
+    src.write_text(body + "void use(struct ip *ip) { in_cksum_update(ip); }\n")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-c", "-I", os.path.join(REPO, "include"),
+                    "-o", str(tmp_path / "order.o"), str(src)], check=True)
+
+
 def test_set_tuning_validation():
     """uinet_cksum_set_tuning accepts each documented knob's range and rejects
     unknown keys and out-of-range values (no device needed)."""

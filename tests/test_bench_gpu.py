@@ -9,6 +9,9 @@
   default ``nccl`` backend: init_process_group("nccl") and the RCCL gather
   (ResultGather with device buffers) run, and the gathered array is checked
   the same way.
+
+Both runs keep the bench's own reference check on (its cpu_baseline leg): the
+JSON line must carry ``bit_identical: true`` over every rank's packets.
 """
 from __future__ import annotations
 
@@ -66,9 +69,10 @@ def _free_port() -> int:
 def test_bench_gpus2_config4_full_shard_gloo(tmp_path, torch_dev):
     path = str(tmp_path / "res.npy")
     d = _bench([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
-                "--save-results", path, "--cpu-baseline", "off"],
+                "--save-results", path],
                {"UINET_BENCH_BACKEND": "gloo"}, timeout=400)
     assert d["n_gpus"] == 2
+    assert d["bit_identical"] is True and d["parity"]["packets"] == 2 * 2097152
     assert d["config"]["workload"].startswith("config4: 4,194,304 x 1500 B")
     assert d["config"]["packets_per_gpu"] == 2097152
     got = np.load(path)
@@ -82,9 +86,10 @@ def test_bench_nccl_world1_rccl_gather(tmp_path, torch_dev):
     d = _bench([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                 "--nproc-per-node=1", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
                 "bench.py", "--gpus", "1", "--steps", "3", "--warmup", "1", "--packets", str(n),
-                "--save-results", path, "--cpu-baseline", "off"],
+                "--save-results", path],
                {"HSA_ENABLE_IPC_MODE_LEGACY": "0"}, timeout=300)
     assert d["n_gpus"] == 1
+    assert d["bit_identical"] is True
     assert "RCCL gather" in d["config"]["parallelism"]
     assert d["config"]["launcher"] == "torch.distributed.run"
     got = np.load(path)

@@ -108,7 +108,8 @@ def test_spans_contig_order(torch_dev, ora, n):
         u.set_tuning("spans_contig", 0)
 
 
-@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0), (2, 1), (2, 0)])
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0), (2, 1), (2, 0),
+                                      (3, 1), (3, 3), (3, 0)])
 def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
     """The persistent two-in-flight span kernel (spans_pipe=1, the default
     for 32 and 64 lanes per packet), the wave-per-packet kernel (2) and the
@@ -138,7 +139,8 @@ def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
         u.set_tuning("blocks_per_cu", 0)
 
 
-@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0), (3, 1), (3, 3),
+                                      (3, 0)])
 def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
     """The strided API on the persistent two-in-flight kernel (spans_pipe=1,
     32 / 64 lanes per packet) and on the one-shot kernel (0), with grids small
@@ -165,6 +167,43 @@ def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
     finally:
         u.set_tuning("spans_pipe", 1)
         u.set_tuning("blocks_per_cu", 0)
+
+
+@pytest.mark.parametrize("pipe", [1, 3])
+def test_spans_far_apart(torch_dev, ora, pipe):
+    """Neighbouring packets (one wave's pair at 32 lanes per packet) that lie
+    4 GiB and more apart in one arena: the lean kernel's loads are relative
+    to one scalar base, and such a pair takes its 64-bit fallback."""
+    torch = torch_dev
+    rng = np.random.default_rng(4242)
+    win = 1 << 16
+    far = (1 << 32) + 4096 + 7  # > 4 GiB between the two windows
+    d = torch.empty(far + win, dtype=torch.uint8, device="cuda")
+    lo, hi = rand_arena(win, 51), rand_arena(win, 52)
+    d[:win].copy_(torch.from_numpy(lo))
+    d[far:far + win].copy_(torch.from_numpy(hi))
+    host = np.concatenate([lo, hi])  # the two windows back to back, for the oracle
+    n = 2000
+    ln = rng.integers(0, 3000, n)
+    ln[::97] = 0
+    o = rng.integers(0, win - 3000, n)
+    side = (np.arange(n) // rng.integers(1, 3)) % 2  # alternate windows, pairs and singles
+    off_dev = np.where(side == 1, far + o, o).astype(np.int64)
+    off_host = np.where(side == 1, win + o, o).astype(np.int64)
+    seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    par = rng.integers(0, 2, n).astype(np.uint8)
+    u.set_tuning("spans_pipe", pipe)
+    try:
+        for hint in (1500, 9000):
+            got = u.cksum_spans(d, dev(torch, off_dev), dev(torch, ln.astype(np.int32)),
+                                seed=dev(torch, seed.view(np.int32)), parity=dev(torch, par),
+                                flags=u.F_UDP, len_hint=hint)
+            want = ora.spans(host, off_host, ln.astype(np.int64), seed, par, u.F_UDP)
+            np.testing.assert_array_equal(host16(got), want)
+    finally:
+        u.set_tuning("spans_pipe", 1)
+        del d
+        torch.cuda.empty_cache()
 
 
 def test_spans_small_packets(torch_dev, ora):

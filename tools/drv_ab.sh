@@ -13,6 +13,7 @@ for rep in $(seq 1 $REPS); do
       pipe) E="UINET_CKSUM_SPANS_PIPE=1";;
       pipe64x2) E="UINET_CKSUM_SPANS_PIPE=1 UINET_CKSUM_SPANS_GEO=1026";;
       wave) E="UINET_CKSUM_SPANS_PIPE=2";;
+      lean) E="UINET_CKSUM_SPANS_PIPE=3";;
       bpc128) E="UINET_CKSUM_SPANS_PIPE=0 UINET_CKSUM_BLOCKS_PER_CU=128";;
       *) echo "unknown variant $v"; exit 2;;
     esac
