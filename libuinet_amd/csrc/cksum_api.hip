@@ -69,7 +69,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
   };
   static const Knob knobs[] = {
       {"blocks_per_cu", &TuningLive::blocks_per_cu, [](int v) { return v >= 0 && v <= 4096; }},
-      {"chains_variant", &TuningLive::chains_variant, [](int v) { return v >= 0 && v <= 2; }},
+      {"chains_variant", &TuningLive::chains_variant, [](int v) { return v >= 0 && v <= 3; }},
       {"chains_pass", &TuningLive::chains_pass, [](int v) { return v >= 2 && v <= 4; }},
       {"chains_long", &TuningLive::chains_long,
        [](int v) { return v == 0 || (v >= 16 && v <= (1 << 24)); }},

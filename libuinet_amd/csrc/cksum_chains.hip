@@ -273,8 +273,7 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
         const uint32_t h = __builtin_amdgcn_readlane(head, s);
         const uint32_t el = __builtin_amdgcn_readlane(eff, s);
         const uint32_t mts = __builtin_amdgcn_readlane(meta, s);
-        const uint8_t* cb = base + (((uint64_t)__builtin_amdgcn_readlane(c0_hi, s) << 32) |
-                                    __builtin_amdgcn_readlane(c0_lo, s));
+        const uint8_t* cb = base + (readlane_u64(c0_lo, c0_hi, s));
         const uint32_t nc = __builtin_amdgcn_readlane(nch, s);
         // chunk k keeps bytes [k ? 0 : h, k < nc - 1 ? 16 : last_end): only the
         // first and last chunks are partial, so no byte position is formed
@@ -307,8 +306,7 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint64_t lm_list = __ballot(nch_l != 0);
       if (lm_list == 0) continue;
       const int lf = (int)__builtin_ctzll(lm_list);
-      const uint64_t R0 = ((uint64_t)__builtin_amdgcn_readlane(c0_hi, lf) << 32) |
-                          __builtin_amdgcn_readlane(c0_lo, lf);
+      const uint64_t R0 = readlane_u64(c0_lo, c0_hi, lf);
       const uint64_t rel = c0 - R0 + (1ull << 31);  // R0 - 2 GiB .. R0 + 2 GiB
       const bool window = __ballot(nch_l != 0 && rel >= (1ull << 32) - (1ull << 16)) == 0;
       const uint32_t q0 = head + 16u * cst;  // < 2^20
@@ -513,6 +511,9 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
+  if (tn.chains_variant == 3)
+    return launch_chains_lean_t(base, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags,
+                                tile, blocks_per_cu(64), long_ch, stream);
 #define LF(P, T, BM)                                                                          \
   hipLaunchKernelGGL((k_chains_pipe<P, T, BM, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, \
                      b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)

@@ -46,6 +46,17 @@ __device__ __forceinline__ uint32_t rot8(uint32_t x) {  // x * 256 mod 65535
 
 __device__ __forceinline__ int clampi(int x, int lo, int hi) { return min(max(x, lo), hi); }
 
+// v_readlane as an unsigned word.  The builtin returns int: OR-ed into the low
+// half of a 64-bit value it sign-extends, and a word with bit 31 set turns the
+// high half to all ones (a bitmap word whose chunk 31 starts a segment; an
+// arena offset of 2 GiB or more).
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t x, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, lane);
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint32_t lo, uint32_t hi, int lane) {
+  return ((uint64_t)readlane_u32(hi, lane) << 32) | readlane_u32(lo, lane);
+}
+
 // Mask of bytes [s, e) of an 8-byte little-endian half-chunk (s, e clamped).
 __device__ __forceinline__ uint64_t byte_mask64(int s, int e) {
   s = clampi(s, 0, 8);

@@ -53,6 +53,12 @@ int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream);
+// k_chains_lean (cksum_chains_lean.hip): tile 8 or 32 packets per wave.
+template <typename OffT, typename LenT>
+int launch_chains_lean_t(const void* base, const OffT* seg_off, const LenT* seg_len,
+                         const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
+                         const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                         int tile, int bpc, uint32_t long_ch, hipStream_t stream);
 int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
                   const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                   const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,

@@ -69,12 +69,6 @@ constexpr MaskWords make_mask_words() {
 }
 __device__ const MaskWords g_mask_words = make_mask_words();
 
-__device__ __forceinline__ void lut_copy(MaskLut& lut) {
-  const u32x4* src = reinterpret_cast<const u32x4*>(g_mask_words.w);
-  for (int i = threadIdx.x; i < 17 * 17; i += blockDim.x) lut.m[i] = src[i];
-  __syncthreads();
-}
-
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 // A wave-uniform value the compiler may not reason about (keeps 32-bit
 // compares of a 64-bit value's halves from being merged back into a 64-bit
@@ -139,6 +133,8 @@ template <int kP>
 struct Geo {
   uint32_t h[kP], e[kP];
   bool far;
+  uint32_t rot;     // Step::rot
+  uint32_t sd[kP];  // Step::sd
 };
 
 template <int G, bool kParity, bool kSeed, bool kStrided>
@@ -276,11 +272,15 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   auto load_step = [&](const Step<kP>& s, u32x4 (&v)[kU]) {
     Geo<kP> z;
     load_round(addr(s, z), 0, v);
+    z.rot = s.rot;
+#pragma unroll
+    for (int g = 0; g < kP; ++g) z.sd[g] = s.sd[g];
     return z;
   };
 
   // A far step's lane partial, every round with per-lane 64-bit addresses.
-  auto far_sum = [&](const Step<kP>& s, const Geo<kP>& z) -> uint32_t {
+  auto far_sum = [&](uint32_t q0, const Geo<kP>& z) -> uint32_t {
+    const Step<kP> s = desc(q0);
     uint32_t chi[kP], clo[kP], lb[kP], emax = 0;
 #pragma unroll
     for (int g = 0; g < kP; ++g) {
@@ -311,8 +311,8 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   // The lane partial of one step: round 0 from registers, later rounds
   // (spans longer than kRound) serially.  Mask-table addresses are 16 x the
   // entry index: 272 x head + 16 x clamp(end - chunk start, 0, 16).
-  auto sum_step = [&](const Step<kP>& s, const Geo<kP>& z, const u32x4 (&v)[kU]) -> uint32_t {
-    if (z.far) return far_sum(s, z);  // wave-uniform, rare
+  auto sum_step = [&](uint32_t q0, const Geo<kP>& z, const u32x4 (&v)[kU]) -> uint32_t {
+    if (z.far) return far_sum(q0, z);  // wave-uniform, rare
     uint32_t E[kP], H[kP], emin = z.e[0], emax = z.e[0];
 #pragma unroll
     for (int g = 0; g < kP; ++g) {
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
     }
     if (emax > kRound) {  // wave-uniform
       Geo<kP> z2;
-      const Addr w = addr(s, z2);
+      const Addr w = addr(desc(q0), z2);
       const uint32_t e0 = gsel(z.e) - pos0;
       for (uint32_t rb = kRound; rb < emax; rb += kRound) {
         u32x4 x[kU];
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
 
   // Packets A (step at q0) and B (step at q0 + S): reduce, fold, rotate, seed,
   // complement and store, once for the 2 * kP packets.
-  auto finish = [&](uint32_t xA, uint32_t xB, const Step<kP>& sA, const Step<kP>& sB,
+  auto finish = [&](uint32_t xA, uint32_t xB, const Geo<kP>& sA, const Geo<kP>& sB,
                     uint32_t q0) {
     uint32_t t;
     if constexpr (kP == 2) {
@@ -393,35 +393,44 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   };
 
   // Steps run two at a time, A and B; the next A's chunks are loaded while B
-  // is summed.  A wave loads no step past the end of the batch: its last one
-  // or two steps leave the loop by their own branch.  Descriptors are fetched
+  // is summed.  The wave knows how many of its steps are live (K), so the
+  // loop body has no exit (an exit that shared code with it made the compiler
+  // wait for the loads in flight) and no step past the end is ever loaded:
+  // the last one or two steps run after the loop.  Descriptors are fetched
   // two steps ahead (clamped to the batch: a clamped fetch is never loaded).
-  u32x4 vA[kU], vB[kU];
-  Step<kP> sA = desc(min(q, (n - 1) & ~(uint32_t)(kP - 1)));
-  Geo<kP> zA = load_step(sA, vA);  // the first step's bytes are in flight ...
-  lut_copy(lut);  // ... while the block copies its mask table (every thread
-                  // reaches this barrier: no exit before it)
-  if (q >= n) return;  // wave-uniform
+  //
+  // The block's mask table: its words are loaded first (L2 hits), then the
+  // first step's chunks, and the table is written to LDS while those are in
+  // flight (the wait before the writes covers only the table's loads).
+  const u32x4* lsrc = reinterpret_cast<const u32x4*>(g_mask_words.w);
+  const u32x4 lw0 = lsrc[threadIdx.x];
+  const u32x4 lw1 = lsrc[min(threadIdx.x + kBlock, 17u * 17u - 1u)];
   const uint32_t qmax = (n - 1) & ~(uint32_t)(kP - 1);  // the last step start
+  u32x4 vA[kU], vB[kU];
+  Geo<kP> zA = load_step(desc(min(q, qmax)), vA);
+  lut.m[threadIdx.x] = lw0;
+  if (threadIdx.x + kBlock < 17u * 17u) lut.m[threadIdx.x + kBlock] = lw1;
+  __syncthreads();  // every thread reaches this barrier: no exit before it
+  if (q >= n) return;  // wave-uniform
+  const uint32_t K = (n - q + S - 1) / S;  // live steps of this wave, >= 1
   Step<kP> sB = desc(min(q + S, qmax));
-  for (;;) {
-    if (q + S >= n) {
-      finish(sum_step(sA, zA, vA), 0u, sA, sA, q);
-      break;
-    }
-    const Geo<kP> zB = load_step(sB, vB);  // step q + S in flight while step q is summed
-    const Step<kP> sC = desc(min(q + 2 * S, qmax));
-    const uint32_t xA = sum_step(sA, zA, vA);
-    if (q + 2 * S >= n) {
-      finish(xA, sum_step(sB, zB, vB), sA, sB, q);
-      break;
-    }
-    zA = load_step(sC, vA);  // step q + 2S in flight while step q + S is summed
-    const Step<kP> sD = desc(min(q + 3 * S, qmax));
-    finish(xA, sum_step(sB, zB, vB), sA, sB, q);
+  uint32_t k = 0;
+  for (; k + 2 < K; k += 2) {  // steps k, k + 1 and k + 2 are live
+    const Geo<kP> zB = load_step(sB, vB);  // step k + 1 in flight while step k is summed
+    const Step<kP> sC = desc(q + 2 * S);
+    const uint32_t xA = sum_step(q, zA, vA);
+    const Geo<kP> zC = load_step(sC, vA);  // step k + 2 in flight while k + 1 is summed
+    sB = desc(min(q + 3 * S, qmax));
+    finish(xA, sum_step(q + S, zB, vB), zA, zB, q);
+    zA = zC;
     q += 2 * S;
-    sA = sC;
-    sB = sD;
+  }
+  if (k + 1 < K) {  // two live steps left
+    const Geo<kP> zB = load_step(sB, vB);
+    const uint32_t xA = sum_step(q, zA, vA);
+    finish(xA, sum_step(q + S, zB, vB), zA, zB, q);
+  } else {  // one
+    finish(sum_step(q, zA, vA), 0u, zA, zA, q);
   }
 }
 

@@ -138,7 +138,7 @@ def test_set_tuning_validation():
           ("chains_pass", 4), ("chains_long", 0), ("chains_long", 16), ("chains_tile", 8),
           ("xcd_remap", 0), ("spans_lut", 1), ("host_threads", 64), ("walk_prefetch", 0),
           ("walk_prefetch", 2), ("spans_contig", 1), ("spans_geo", 0), ("spans_geo", 32 * 16 + 3), ("spans_sdesc", 0), ("host_group", 4), ("host_pin", 1)]
-    bad = [("blocks_per_cu", -1), ("chains_variant", 3), ("chains_pass", 8), ("chains_long", 15),
+    bad = [("blocks_per_cu", -1), ("chains_variant", 4), ("chains_pass", 8), ("chains_long", 15),
            ("chains_tile", 64), ("xcd_remap", 2), ("host_threads", 0), ("walk_prefetch", 3),
            ("spans_contig", 2), ("spans_geo", 16 * 16 + 6), ("spans_geo", 5), ("spans_sdesc", 2), ("host_group", 0), ("host_pin", 2), ("no_such_knob", 1)]
     try:

@@ -83,7 +83,7 @@ def test_chains32_len_skip_seed(torch_dev, ora, hint):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,long_ch,tile", [(0, 128, 0), (0, 16, 8), (0, 0, 32), (1, 128, 0), (2, 128, 0),
+@pytest.mark.parametrize("variant,long_ch,tile", [(0, 128, 0), (0, 16, 8), (0, 0, 32), (1, 128, 0), (2, 128, 0), (3, 128, 0), (3, 16, 8), (3, 0, 32),
                                                    (2, 16, 8), (2, 0, 32)])
 def test_chains32_long_and_many_segments(torch_dev, ora, variant, long_ch, tile):
     """Segments up to 65535 B (the u16 limit) mixed with 0..3-B ones, chains of

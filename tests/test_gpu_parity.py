@@ -688,7 +688,7 @@ def test_zero_copy_pipeline_ring(torch_dev, ora, host_threads):
         np.testing.assert_array_equal(got[("hdr", k)], want_hdr)
 
 
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 3])
 @pytest.mark.parametrize("long_ch,tile", [(0, 32), (16, 8), (16, 32), (64, 0), (200, 8)])
 def test_chains_long_segments(torch_dev, ora, long_ch, tile, variant):
     """Chains mixing short and long (wave-streamed) segments, with len/skip
@@ -728,7 +728,7 @@ def test_chains_long_segments(torch_dev, ora, long_ch, tile, variant):
         u.set_tuning("chains_variant", 0)
 
 
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 3])
 @pytest.mark.parametrize("long_ch", [0, 200])
 def test_chains_full_rounds(torch_dev, ora, long_ch, variant):
     """Descriptor rounds whose chunk list is longer than 4096 chunks: 64
@@ -765,7 +765,7 @@ def test_chains_full_rounds(torch_dev, ora, long_ch, variant):
         u.set_tuning("chains_tile", 0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_chains_kernel_variants(torch_dev, ora, variant):
     """The chain kernels (0 chunk stream, 1 serial walk, 2 chunk stream with
     the bitmap segment lookup) on chains of 0..150 segments with
@@ -817,15 +817,18 @@ def test_chains_beyond_4gib_window(torch_dev, ora):
     pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
     s = int(pkt_seg[-1])
     seg_len = rng.integers(0, 300, s)
+    # every 40th segment is long (2-9 KB: the wave-streamed path), at offsets
+    # on both sides of 2 GiB and 4 GiB (64-bit bases whose low word has bit 31)
+    seg_len[::40] = rng.integers(2048, 9000, seg_len[::40].size)
     pkt = np.repeat(np.arange(n), nseg)
-    tile_base = rng.integers(0, size - (2 << 20), n // 32 + 1)
+    tile_base = rng.integers(0, size - (2 << 20) - 9100, n // 32 + 1)
     local = tile_base[pkt // 32] + rng.integers(0, 1 << 20, s)
-    scattered = rng.integers(0, size - 512, s)
+    scattered = rng.integers(0, size - 9100, s)
     seg_off = np.where((pkt // 32) % 2 == 0, local, scattered).astype(np.int64)
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     skip = np.full(n, 3, np.int64)
     want = ora.chains(host, seg_off, seg_len, pkt_seg, skip=skip, seed=seed)
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, 3):
         u.set_tuning("chains_variant", variant)
         try:
             got = u.cksum_chains(d, dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
