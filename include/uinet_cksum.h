@@ -174,6 +174,8 @@ int uinet_cksum_device_ok(void);
  *                     16 chains in lockstep (never changes results)
  *   "host_group"      zero-copy host-mbuf batches: chunks per host thread in
  *                     one pipeline group (1..64, default 1)
+ *   "multi_gather"    uinet_cksum_spans_multi: 0 = one RCCL gather when it
+ *                     applies (default), 1 = always peer copies
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
  * (0|1|2, or serial), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
@@ -355,10 +357,17 @@ struct uinet_cksum_shard {
 /* Folds every shard on its own device (the span kernel, as
  * uinet_cksum_spans) and gathers the 16-bit results into root_out, a device
  * pointer on root_device: shard k's results start at the sum of the n of
- * shards 0..k-1.  The gather is a peer copy over xGMI (on-device when a
- * shard lives on root_device).  Returns when every result is in root_out. */
+ * shards 0..k-1.  The gather is ONE RCCL gather over xGMI (an in-process
+ * communicator over the shards' devices, built on first use per device list;
+ * RCCL is loaded at run time) when every shard has its own device and one of
+ * them is root_device; otherwise (or with the "multi_gather" knob at 1, or
+ * without RCCL) peer copies over xGMI.  Returns when every result is in
+ * root_out. */
 int uinet_cksum_spans_multi(const struct uinet_cksum_shard *shards, int nshards,
     uint32_t flags, uint32_t len_hint, int root_device, uint16_t *root_out);
+/* How the calling thread's last uinet_cksum_spans_multi gathered: 1 RCCL,
+ * 0 peer copies, -1 no call yet. */
+int uinet_cksum_multi_last_gather(void);
 
 /* A host-mbuf batch (in_cksum_skip_batch semantics) over ndev devices: the
  * packets are cut into ndev contiguous ranges of about equal summed bytes

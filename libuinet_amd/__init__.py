@@ -52,7 +52,7 @@ EXPORTED_SYMBOLS = (
     "uinet_cksum_register_host", "uinet_cksum_unregister_host",
     "uinet_cksum_rx_offload", "uinet_cksum_tx_offload",
     "in6_cksum", "in6_cksum_pseudo", "in6_cksum_batch",
-    "uinet_cksum_spans_multi", "in_cksum_skip_batch_multi",
+    "uinet_cksum_spans_multi", "uinet_cksum_multi_last_gather", "in_cksum_skip_batch_multi",
 )
 
 # Driver offload status bits (include/uinet_cksum.h section 2d).
@@ -117,6 +117,7 @@ def lib() -> ctypes.CDLL:
         "in6_cksum_pseudo": (_i32, [_vp, _u32, _u8, _u16]),
         "in6_cksum_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32]),
         "uinet_cksum_spans_multi": (_i32, [_vp, _i32, _u32, _u32, _i32, _vp]),
+        "uinet_cksum_multi_last_gather": (_i32, []),
         "in_cksum_skip_batch_multi": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i32]),
     }
     for name, (res, args) in sig.items():
@@ -421,6 +422,12 @@ def cksum_spans_multi(shards, root_device: int = 0, out=None, flags: int = 0,
     _check("uinet_cksum_spans_multi", lib().uinet_cksum_spans_multi(
         ctypes.addressof(arr), len(shards), flags, len_hint, root_device, _dp(out)))
     return out
+
+
+def multi_last_gather() -> int:
+    """How this thread's last cksum_spans_multi gathered: 1 one RCCL gather,
+    0 peer copies, -1 no call yet."""
+    return lib().uinet_cksum_multi_last_gather()
 
 
 def in_cksum_skip_batch_multi(devices, heads, length, skip) -> np.ndarray:

@@ -58,7 +58,8 @@ int check_launch() { return record_hip(hipGetLastError()); }
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_variant{0}, chains_pass{2}, host_threads{8},
       chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1}, walk_prefetch{1},
-      spans_contig{0}, spans_geo{0}, spans_sdesc{1}, spans_pipe{1}, host_group{1}, host_pin{0};
+      spans_contig{0}, spans_geo{0}, spans_sdesc{1}, spans_pipe{1}, host_group{1}, host_pin{0},
+      multi_gather{0};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -85,6 +86,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
       {"host_group", &TuningLive::host_group, [](int v) { return v >= 1 && v <= 64; }},
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
+      {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -104,7 +106,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_CONTIG", "spans_contig"},
         {"UINET_CKSUM_SPANS_GEO", "spans_geo"},         {"UINET_CKSUM_SPANS_SDESC", "spans_sdesc"},
         {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},       {"UINET_CKSUM_HOST_GROUP", "host_group"},
-        {"UINET_CKSUM_HOST_PIN", "host_pin"},
+        {"UINET_CKSUM_HOST_PIN", "host_pin"},          {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -140,6 +142,7 @@ Tuning tuning() {
   x.spans_pipe = ld(t.spans_pipe);
   x.host_group = ld(t.host_group);
   x.host_pin = ld(t.host_pin);
+  x.multi_gather = ld(t.multi_gather);
   return x;
 }
 

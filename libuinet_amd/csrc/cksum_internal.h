@@ -32,6 +32,7 @@ struct Tuning {
   int host_group;      // zero-copy host batches: chunks per thread in one pipeline
                        // group (a pool pass walks a group while the GPU folds the last)
   int host_pin;        // host pool helpers pinned to CPUs 1.. of the process mask (0/1)
+  int multi_gather;    // uinet_cksum_spans_multi: 0 RCCL gather when it applies, 1 peer copies
 };
 Tuning tuning();
 // True when G * 16 + U names a compiled span-kernel geometry.

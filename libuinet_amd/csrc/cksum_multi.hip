@@ -1,22 +1,32 @@
 // Multi-device batches (include/uinet_cksum.h section 2e).
 //
 // The checksum has no cross-packet term, so a batch shards across GPUs with
-// no data-path exchange: one host thread per shard, each with its own stream
-// on the shard's device, and the only traffic between devices is the 2-B
-// result per packet.  For device-resident shards those results are gathered
-// on the root device by peer copies over xGMI (hipMemcpyPeerAsync, peer
-// access enabled once per device pair); for host-mbuf batches every shard
-// writes its own slice of the caller's host array.  This is the C-ABI form of
-// the bench's torch.distributed layout (one process per GPU, RCCL gather):
-// it serves a libuinet process whose RX/TX kthreads
-// (/root/reference/lib/libuinet/uinet_if_netmap.c:1652-1665) call into one
-// library on a multi-GPU host, without torch or a launcher.
+// no data-path exchange, and the only traffic between devices is the 2-B
+// result per packet.  For device-resident shards those results meet on the
+// root device in ONE RCCL gather over xGMI: an in-process communicator over
+// the shards' devices (ncclCommInitAll, cached per device list), every
+// shard's kernel on its device's stream, then one grouped ncclGather (in
+// place on the root when the shards are equal-sized).  RCCL is loaded with
+// dlopen on first use, so the drop-in library has no hard dependency on it;
+// when it cannot be loaded, when a device appears twice in the list, or when
+// the root device holds no shard, the results are gathered by peer copies
+// (hipMemcpyPeerAsync over xGMI, one host thread and stream per shard).  For
+// host-mbuf batches every shard writes its own slice of the caller's host
+// array.  This is the C-ABI form of the bench's torch.distributed layout (one
+// process per GPU, RCCL gather): it serves a libuinet process whose RX/TX
+// kthreads (/root/reference/lib/libuinet/uinet_if_netmap.c:1652-1665) call
+// into one library on a multi-GPU host, without torch or a launcher.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "cksum_internal.h"
@@ -89,6 +99,147 @@ int shard_spans(const uinet_cksum_shard& sh, uint32_t flags, uint32_t len_hint, 
   return record_hip(hipStreamSynchronize(c.stream));
 }
 
+// --- RCCL, loaded at first use ------------------------------------------
+struct Rccl {
+  bool ok = false;
+  decltype(&ncclCommInitAll) init = nullptr;
+  decltype(&ncclGather) gather = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+};
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.init = reinterpret_cast<decltype(x.init)>(dlsym(h, "ncclCommInitAll"));
+    x.gather = reinterpret_cast<decltype(x.gather)>(dlsym(h, "ncclGather"));
+    x.group_start = reinterpret_cast<decltype(x.group_start)>(dlsym(h, "ncclGroupStart"));
+    x.group_end = reinterpret_cast<decltype(x.group_end)>(dlsym(h, "ncclGroupEnd"));
+    x.ok = x.init && x.gather && x.group_start && x.group_end;
+    return x;
+  }();
+  return r;
+}
+
+// One communicator per distinct device list (rank k = list entry k), with a
+// stream and a result buffer per rank and the root's padding buffer.  Built
+// once (ncclCommInitAll costs ~100 ms) and kept for the process; calls that
+// use the same list serialise on its mutex.
+struct CommSet {
+  std::mutex mu;
+  bool ok = false;
+  std::vector<int> dev;
+  std::vector<ncclComm_t> comm;
+  std::vector<hipStream_t> stream;
+  std::vector<uint16_t*> buf;  // rank k's results (capacity cap each)
+  uint64_t cap = 0;
+  uint16_t* pad = nullptr;     // root: ranks x cap, for unequal shards
+  uint64_t pad_cap = 0;
+};
+CommSet* comm_set(const std::vector<int>& dev) {
+  static std::mutex mu;
+  static std::map<std::vector<int>, CommSet*>* sets = new std::map<std::vector<int>, CommSet*>;
+  std::lock_guard<std::mutex> g(mu);
+  CommSet*& cs = (*sets)[dev];
+  if (cs) return cs->ok ? cs : nullptr;
+  cs = new CommSet;  // kept even when init fails: the next call falls back at once
+  cs->dev = dev;
+  cs->comm.assign(dev.size(), nullptr);
+  if (rccl().init(cs->comm.data(), (int)dev.size(), dev.data()) != ncclSuccess) return nullptr;
+  cs->stream.assign(dev.size(), nullptr);
+  cs->buf.assign(dev.size(), nullptr);
+  for (size_t k = 0; k < dev.size(); k++) {
+    if (hipSetDevice(dev[k]) != hipSuccess ||
+        hipStreamCreateWithFlags(&cs->stream[k], hipStreamNonBlocking) != hipSuccess)
+      return nullptr;
+  }
+  cs->ok = true;
+  return cs;
+}
+
+thread_local int t_last_gather = -1;  // 1 RCCL, 0 peer copies (uinet_cksum_multi_last_gather)
+
+// The RCCL path; returns 1 when it does not apply (the caller falls back).
+int spans_multi_rccl(const uinet_cksum_shard* shards, int ns, uint32_t flags, uint32_t len_hint,
+                     int root_device, uint16_t* root_out, const std::vector<uint64_t>& at) {
+  if (!rccl().ok || tuning().multi_gather != 0) return 1;
+  std::vector<int> dev((size_t)ns);
+  int root = -1;
+  uint64_t nmax = 0;
+  bool equal = true;
+  for (int k = 0; k < ns; k++) {
+    dev[(size_t)k] = shards[k].device;
+    if (shards[k].device == root_device) root = k;
+    nmax = std::max<uint64_t>(nmax, shards[k].n);
+    equal = equal && shards[k].n == shards[0].n;
+  }
+  std::vector<int> sorted = dev;
+  std::sort(sorted.begin(), sorted.end());
+  if (root < 0 || std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end() || nmax == 0)
+    return 1;
+  CommSet* cs = comm_set(dev);
+  if (!cs) return 1;
+  std::lock_guard<std::mutex> g(cs->mu);
+  int rc = 0;
+  if (nmax > cs->cap) {
+    for (int k = 0; k < ns; k++) {
+      if ((rc = record_hip(hipSetDevice(dev[(size_t)k])))) return rc;
+      if (cs->buf[(size_t)k]) (void)hipFree(cs->buf[(size_t)k]);
+      cs->buf[(size_t)k] = nullptr;
+      if ((rc = record_hip(hipMalloc((void**)&cs->buf[(size_t)k], 2 * nmax)))) return rc;
+    }
+    cs->cap = nmax;
+  }
+  const uint64_t need = equal ? 0 : (uint64_t)ns * nmax;
+  if (need > cs->pad_cap) {
+    if ((rc = record_hip(hipSetDevice(root_device)))) return rc;
+    if (cs->pad) (void)hipFree(cs->pad);
+    cs->pad = nullptr;
+    if ((rc = record_hip(hipMalloc((void**)&cs->pad, 2 * need)))) return rc;
+    cs->pad_cap = need;
+  }
+  // every shard's kernel on its device's stream; with equal shards the root
+  // folds straight into its slice of root_out and gathers in place there
+  for (int k = 0; k < ns; k++) {
+    const uinet_cksum_shard& sh = shards[k];
+    if ((rc = record_hip(hipSetDevice(sh.device)))) return rc;
+    uint16_t* o = (equal && k == root) ? root_out + at[(size_t)k] : cs->buf[(size_t)k];
+    if (sh.n &&
+        (rc = launch_spans(sh.base, sh.off, sh.len, sh.seed, sh.parity, o, sh.n, flags, len_hint,
+                           cs->stream[(size_t)k])))
+      return rc;
+  }
+  uint16_t* recv = equal ? root_out : cs->pad;
+  if (rccl().group_start() != ncclSuccess) return UINET_CKSUM_EHIP;
+  for (int k = 0; k < ns; k++) {
+    const void* send = (equal && k == root) ? (const void*)(root_out + at[(size_t)k])
+                                            : (const void*)cs->buf[(size_t)k];
+    if (rccl().gather(send, k == root ? (void*)recv : nullptr, 2 * nmax, ncclUint8, root,
+                      cs->comm[(size_t)k], cs->stream[(size_t)k]) != ncclSuccess) {
+      (void)rccl().group_end();
+      return UINET_CKSUM_EHIP;
+    }
+  }
+  if (rccl().group_end() != ncclSuccess) return UINET_CKSUM_EHIP;
+  if (!equal) {  // unequal shards: compact the padded slots on the root
+    if ((rc = record_hip(hipSetDevice(root_device)))) return rc;
+    for (int k = 0; k < ns; k++)
+      if (shards[k].n &&
+          (rc = record_hip(hipMemcpyAsync(root_out + at[(size_t)k], cs->pad + (uint64_t)k * nmax,
+                                          2 * (size_t)shards[k].n, hipMemcpyDeviceToDevice,
+                                          cs->stream[(size_t)root]))))
+        return rc;
+  }
+  for (int k = 0; k < ns; k++) {
+    if ((rc = record_hip(hipSetDevice(dev[(size_t)k])))) return rc;
+    if ((rc = record_hip(hipStreamSynchronize(cs->stream[(size_t)k])))) return rc;
+  }
+  t_last_gather = 1;
+  return 0;
+}
+
 int first_error(const std::vector<int>& rc) {
   for (int r : rc)
     if (r) return r;
@@ -119,6 +270,14 @@ int uinet_cksum_spans_multi(const struct uinet_cksum_shard* shards, int nshards,
   }
   int prev = 0;
   (void)hipGetDevice(&prev);
+  if (nshards > 0) {
+    const int r = spans_multi_rccl(shards, nshards, flags, len_hint, root_device, root_out, at);
+    if (r != 1) {
+      (void)hipSetDevice(prev);
+      return r;
+    }
+  }
+  t_last_gather = 0;
   std::vector<int> rc((size_t)nshards, 0);
   shard_pool().run(nshards, nshards, [&](int k) {
     int keep = 0;
@@ -129,6 +288,8 @@ int uinet_cksum_spans_multi(const struct uinet_cksum_shard* shards, int nshards,
   (void)hipSetDevice(prev);
   return first_error(rc);
 }
+
+int uinet_cksum_multi_last_gather(void) { return t_last_gather; }
 
 int in_cksum_skip_batch_multi(const int* devices, int ndev, struct mbuf* const* m, const int* len,
                               const int* skip, unsigned short* out, int n) {

@@ -87,10 +87,11 @@ __device__ __forceinline__ uint64_t sld64(const uint64_t* p) {
 __device__ __forceinline__ uint32_t sld32(const uint32_t* p) {
   return rfl(*(const __attribute__((address_space(4))) uint32_t*)(uintptr_t)p);
 }
-// The byte at p, from the aligned dword that holds it (never crosses a page).
-__device__ __forceinline__ uint32_t sld8(const uint8_t* p) {
+// The aligned dword that holds the byte at p (never crosses a page); the
+// byte is (word >> 8 * (p & 3)) & 0xff.
+__device__ __forceinline__ uint32_t sld8w(const uint8_t* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  return (sld32(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)) >> (8 * (a & 3))) & 0xffu;
+  return sld32(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3));
 }
 
 // Four dot2 against (1, 1): both 16-bit halves of every word added into acc.
@@ -112,23 +113,22 @@ __device__ __forceinline__ uint32_t add_ror(uint32_t x) {
   return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x120 + kN, 0xf, 0xf, false);
 }
 
-// One step of a wave: the descriptors of its kP packets (one per lane group),
-// in SGPRs.  o / l are the span offset from `base` and its length (an empty
-// span borrows its neighbour's offset, or 0, so that its re-read chunk is
-// one the wave reads anyway); rot holds the packets' rotation bits
-// (address parity != logical parity, in_cksum.c:222-225) already placed at
-// the reduction rows of an A step (G = 32: rows 0 / 2; G = 64: rows 0, 1);
-// sd the folded seeds (the in_cksum_pseudo_header sum, in_cksum.c:241-276).
+// One step of a wave: the raw descriptors of its kP packets (one per lane
+// group) as its scalar loads return them, in SGPRs.
 template <int kP>
 struct Step {
-  uint64_t o[kP];
-  uint32_t l[kP];
-  uint32_t rot;
-  uint32_t sd[kP];
+  uint64_t o[kP];   // span offsets from `base`
+  uint32_t l[kP];   // lengths
+  uint32_t sd[kP];  // raw seeds
+  uint32_t lp[kP];  // the aligned dword holding the parity byte, and its shift
+  uint32_t q0;      // the step's first packet
 };
-// What a step's sum needs from its load: head (span start inside its first
-// chunk) and end (head + len) per packet, and whether the pair lies too far
-// apart for 32-bit lane offsets from one scalar base.
+// What a step's sum needs, derived when it is loaded: head (span start inside
+// its first chunk) and end (head + len) per packet; whether the pair lies too
+// far apart for 32-bit lane offsets from one scalar base; the rotation bits
+// (address parity != logical parity, in_cksum.c:222-225) placed at the
+// reduction rows of an A step (G = 32: rows 0 / 2; G = 64: rows 0, 1); the
+// folded seeds (the in_cksum_pseudo_header sum, in_cksum.c:241-276).
 template <int kP>
 struct Geo {
   uint32_t h[kP], e[kP];
@@ -189,41 +189,26 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   const __amdgpu_buffer_rsrc_t out_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(2u * n), 0x00020000);
 
-  // Descriptors of the step at q0 (< n; q0 even when kP = 2, so a pair's
-  // offsets and lengths are adjacent words).
+  // Descriptors of the step at q0 (< n; q0 even when kP = 2): scalar loads
+  // only, no dependent arithmetic and no branch (the second packet's index is
+  // clamped to the batch), so issuing them never waits for them; everything
+  // derived from them is computed where the step is loaded.
   auto desc = [&](uint32_t q0) {
     Step<kP> s;
-    const bool two = kP == 2 && q0 + 1 < n;
-    if constexpr (kStrided) {
-      s.o[0] = (uint64_t)q0 * stride;
-      s.l[0] = slen;
-      if constexpr (kP == 2) {
-        s.o[1] = s.o[0] + stride;
-        s.l[1] = two ? slen : 0u;
-      }
-    } else {
-      s.o[0] = sld64(off + q0);
-      s.l[0] = sld32(len + q0);
-      if constexpr (kP == 2) {
-        s.o[1] = two ? sld64(off + q0 + 1) : s.o[0];
-        s.l[1] = two ? sld32(len + q0 + 1) : 0u;
-      }
-    }
-    uint32_t b[kP];
 #pragma unroll
     for (int g = 0; g < kP; ++g) {
-      const uint32_t lp = kParity ? (g == 0 || two ? sld8(parity + q0 + g) : 0u) : 0u;
-      b[g] = (lp ^ boff ^ (uint32_t)s.o[g]) & 1u;
-      s.sd[g] = kSeed ? (g == 0 || two ? fold16_32(sld32(seed + q0 + g)) : 0u) : 0u;
+      const uint32_t qg = min(q0 + (uint32_t)g, n - 1);
+      if constexpr (kStrided) {
+        s.o[g] = (uint64_t)qg * stride;
+        s.l[g] = slen;
+      } else {
+        s.o[g] = sld64(off + qg);
+        s.l[g] = sld32(len + qg);
+      }
+      s.sd[g] = kSeed ? sld32(seed + qg) : 0u;
+      s.lp[g] = kParity ? sld8w(parity + qg) : 0u;
     }
-    if constexpr (kP == 2) {
-      s.rot = b[0] | (b[1] << 2);
-      if (!s.l[0]) s.o[0] = s.l[1] ? s.o[1] : 0;
-      if (!s.l[1]) s.o[1] = s.o[0];
-    } else {
-      s.rot = b[0] * 3u;
-      if (!s.l[0]) s.o[0] = 0;
-    }
+    s.q0 = q0;
     return s;
   };
 
@@ -235,8 +220,35 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
     const uint8_t* sb;
     uint32_t d[kP], lo[kP];
   };
-  auto addr = [&](const Step<kP>& s, Geo<kP>& z) {
+  // Past-the-end packets get length 0; an empty span borrows its neighbour's
+  // offset (or 0), so that its re-read chunk is one the wave reads anyway and
+  // its own (unread) offset is never dereferenced.
+  auto norm = [&](Step<kP> s) {
+#pragma unroll
+    for (int g = 0; g < kP; ++g)
+      if (s.q0 + (uint32_t)g >= n) s.l[g] = 0;
+    if constexpr (kP == 2) {
+      if (!s.l[0]) s.o[0] = s.l[1] ? s.o[1] : 0;
+      if (!s.l[1]) s.o[1] = s.o[0];
+    } else {
+      if (!s.l[0]) s.o[0] = 0;
+    }
+    return s;
+  };
+  auto addr = [&](const Step<kP>& s0, Geo<kP>& z) {
     Addr w;
+    uint32_t b[kP];
+#pragma unroll
+    for (int g = 0; g < kP; ++g) {
+      const uint32_t qg = s0.q0 + (uint32_t)g;
+      const uint32_t lp =
+          kParity ? (s0.lp[g] >> (8 * ((uint32_t)reinterpret_cast<uintptr_t>(parity) + qg))) & 1u
+                  : 0u;
+      b[g] = (lp ^ boff ^ (uint32_t)s0.o[g]) & 1u;
+      z.sd[g] = kSeed && qg < n ? fold16_32(s0.sd[g]) : 0u;
+    }
+    z.rot = kP == 2 ? (b[0] | (b[kP - 1] << 2)) : b[0] * 3u;
+    const Step<kP> s = norm(s0);
     uint32_t lastb[kP];
 #pragma unroll
     for (int g = 0; g < kP; ++g) {
@@ -272,15 +284,12 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   auto load_step = [&](const Step<kP>& s, u32x4 (&v)[kU]) {
     Geo<kP> z;
     load_round(addr(s, z), 0, v);
-    z.rot = s.rot;
-#pragma unroll
-    for (int g = 0; g < kP; ++g) z.sd[g] = s.sd[g];
     return z;
   };
 
   // A far step's lane partial, every round with per-lane 64-bit addresses.
   auto far_sum = [&](uint32_t q0, const Geo<kP>& z) -> uint32_t {
-    const Step<kP> s = desc(q0);
+    const Step<kP> s = norm(desc(q0));
     uint32_t chi[kP], clo[kP], lb[kP], emax = 0;
 #pragma unroll
     for (int g = 0; g < kP; ++g) {

@@ -57,6 +57,35 @@ def test_spans_multi_gather(torch_dev, ora, nshards):
     got = u.cksum_spans_multi(shards, root_device=0, len_hint=1500)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(got.cpu().view(torch.int16).numpy().view(np.uint16), want)
+    # one shard per device (here: the one device) takes the in-process RCCL
+    # gather; a device that appears twice takes the peer copies
+    assert u.multi_last_gather() == (1 if nshards == 1 else 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gather", [0, 1])
+def test_spans_multi_rccl_single_device(torch_dev, ora, gather):
+    """The RCCL branch of uinet_cksum_spans_multi on a one-device list (a
+    communicator of one rank, the gather in place on the root) against the
+    peer-copy branch (knob multi_gather=1), config-2 shaped, twice in a row
+    (the second call reuses the cached communicator)."""
+    torch = torch_dev
+    arena = aligned_empty(1500 * 40000 + 64)
+    splitmix64_bytes(arena.size, 7, out=arena)
+    off = 1500 * np.arange(40000, dtype=np.int64)
+    ln = np.full(40000, 1500, np.int32)
+    want = ora.spans(arena, off, ln)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()  # noqa: E731
+    sh = [dict(base=d(arena), off=d(off), length=d(ln))]
+    u.set_tuning("multi_gather", gather)
+    try:
+        for _ in range(2):
+            got = u.cksum_spans_multi(sh, root_device=0, len_hint=1500)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(got.cpu().view(torch.int16).numpy().view(np.uint16), want)
+            assert u.multi_last_gather() == (1 if gather == 0 else 0)
+    finally:
+        u.set_tuning("multi_gather", 0)
 
 
 @pytest.mark.gpu
