@@ -60,6 +60,11 @@ int launch_chains_lean_t(const void* base, const OffT* seg_off, const LenT* seg_
                          const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                          const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
                          int tile, int bpc, uint32_t long_ch, hipStream_t stream);
+// k_spans_lane (cksum_spans.hip): one lane per packet, for small packets.
+int launch_spans_lane(const void* base, const uint64_t* off, const uint32_t* len,
+                      const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                      uint32_t flags, bool strided, uint64_t stride, uint32_t slen, int blocks_cu,
+                      hipStream_t stream);
 int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
                   const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                   const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,

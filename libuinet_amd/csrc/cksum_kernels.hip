@@ -476,6 +476,9 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   // (profiles/r02/ab_sdesc/): vector descriptors at 256 / CU 0.2192 ms,
   // scalar at 256 / CU 0.2167, scalar at 512 / CU 0.2086 (+5.1 %), 4096 / CU
   // 0.2095; on a slower stretch of the same box +1.4 %.
+  if (tuning().spans_pipe == 3 && geo.g == 4)
+    return launch_spans_lane(base, off, len, seed, parity, out, n, flags, false, 0, 0,
+                             blocks_per_cu(32), stream);
   const bool sdesc = tuning().spans_sdesc && geo.g >= 32;
   if (sdesc && tuning().spans_pipe == 3 && geo.u == 3)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, false, 0, 0,
@@ -551,6 +554,9 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   geo = geometry_override(geo);
   // one packet per group suits long packets; small ones want groups that
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
+  if (tuning().spans_pipe == 3 && geo.g == 4)
+    return launch_spans_lane(base, nullptr, nullptr, seed, nullptr, out, n, flags, true,
+                             pkt_stride, len, blocks_per_cu(32), stream);
   if (geo.g >= 32 && tuning().spans_pipe == 3 && geo.u == 3)
     return launch_spans_lean(base, nullptr, nullptr, seed, nullptr, out, n, flags, geo.g, true,
                              pkt_stride, len, blocks_per_cu(128), stream);

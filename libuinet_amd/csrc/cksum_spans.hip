@@ -443,7 +443,134 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   }
 }
 
+// k_spans_lane: one LANE per packet, for small packets (<= 64 B; config 2s
+// shapes).  Round 2 found 64-B packets bound by per-packet vector work, not
+// by bytes in flight (profiles/r02/ab_small/): with 4 lanes per packet every
+// packet pays its mask-table sums, a 2-step butterfly, the fold, rotation,
+// complement and store, for 64 bytes.  Here each lane folds its own packet:
+// no cross-lane reduction at all, and every per-packet instruction serves 64
+// packets.  A lane loads its packet's kLU 16-byte chunks (5 hold any span of
+// <= 65 B at any alignment); one load instruction touches 64 packets' chunks
+// (64 x 16 B over 4 KiB; the wave's kLU loads consume every byte of those
+// lines, through L1), its descriptors are one coalesced vector load per array.
+// A chunk slot that no lane needs masked (aligned 64-B packets: all but the
+// last) skips the mask table.  Longer spans (ragged batches) finish with
+// further rounds of kLU chunks.
+constexpr int kLU = 5;
+
+template <bool kParity, bool kSeed, bool kStrided>
+__global__ __launch_bounds__(kBlock) void k_spans_lane(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed,
+    const uint8_t* __restrict__ parity, uint16_t* __restrict__ out, uint32_t n, uint32_t flags,
+    uint64_t stride, uint32_t slen) {
+  __shared__ MaskLut lut;
+  const u32x4* lsrc = reinterpret_cast<const u32x4*>(g_mask_words.w);
+  lut.m[threadIdx.x] = lsrc[threadIdx.x];
+  if (threadIdx.x + kBlock < 17u * 17u) lut.m[threadIdx.x + kBlock] = lsrc[threadIdx.x + kBlock];
+  __syncthreads();  // every thread reaches this barrier: no exit before it
+  const uint32_t boff = (uint32_t)(reinterpret_cast<uintptr_t>(base) & 15);
+  const uint8_t* abase = base - boff;
+  const uint32_t step = gridDim.x * kBlock;
+  // descriptors one iteration ahead, behind the data loads (index clamped to
+  // the batch, so the prefetch is unconditional)
+  auto fetch = [&](uint32_t q, uint64_t& o, uint32_t& l) {
+    const uint32_t qc = min(q, n - 1);
+    if constexpr (kStrided) {
+      o = (uint64_t)qc * stride;
+      l = slen;
+    } else {
+      o = off[qc];
+      l = len[qc];
+    }
+  };
+  uint64_t o_next;
+  uint32_t l_next;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t p0 = blockIdx.x * kBlock + (threadIdx.x & ~63u);
+  fetch(p0 + lane, o_next, l_next);
+  for (; p0 < n; p0 += step) {
+    const uint32_t q = p0 + lane;  // this lane's packet
+    const bool live = q < n;
+    const uint32_t qc = live ? q : n - 1;
+    const uint64_t o = o_next;
+    uint32_t l = l_next;
+    if (!live) l = 0;
+    const uint64_t oa = o + boff;
+    const uint32_t head = l ? (uint32_t)oa & 15u : 0u;
+    const uint32_t end = head + l;  // bytes [head, end) from the first chunk
+    const uint32_t lastb = (max(end, 1u) - 1u) & ~15u;  // 16 x the last chunk
+    // an empty span (or a dead lane) re-reads the arena's first chunk
+    const uint8_t* c0 = l ? abase + (oa - head) : abase;
+    u32x4 v[kLU];
+#pragma unroll
+    for (int j = 0; j < kLU; ++j) v[j] = load_chunk(c0 + min(16u * j, lastb));
+    fetch(p0 + step + lane, o_next, l_next);
+    const uint32_t sd = kSeed && live ? seed[qc] : 0u;
+    const uint32_t lp = kParity && live ? parity[qc] : 0u;
+    // chunk j keeps bytes [head - 16 j, end - 16 j): masked unless the whole
+    // wave has it whole (wave-uniform ballots)
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < kLU; ++j) {
+      const int s_j = (int)head - 16 * j, e_j = (int)end - 16 * j;
+      if (__ballot(!(s_j <= 0 && e_j >= 16)) == 0)
+        acc = dot_acc(v[j], acc);
+      else
+        acc = dot_acc_masked(v[j], lut.m[MaskLut::index(s_j, e_j)], acc);
+    }
+    if (__ballot(end > 16u * kLU)) {  // spans longer than kLU chunks
+      for (uint32_t k0 = kLU; 16u * k0 < end || __ballot(16u * k0 < end); k0 += kLU) {
+        u32x4 w[kLU];
+#pragma unroll
+        for (int j = 0; j < kLU; ++j) w[j] = load_chunk(c0 + min(16u * (k0 + j), lastb));
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < kLU; ++j) {
+          const int b = 16 * (int)(k0 + j);
+          r = dot_acc_masked(w[j], lut.m[MaskLut::index((int)head - b, (int)end - b)], r);
+        }
+        acc = fold16_32(acc) + r;
+      }
+    }
+    uint32_t x = fold16_32(acc);
+    x = fold16_32(x << (8u * ((lp ^ (uint32_t)oa) & 1u)));  // x * 256^rot mod 65535
+    if (kSeed) x = fold16_32(x + fold16_32(sd));
+    uint32_t res = x;
+    if (!(flags & UINET_CKSUM_F_NO_COMPLEMENT)) {
+      res = ~x & 0xffffu;
+      if ((flags & UINET_CKSUM_F_UDP) && res == 0) res = 0xffff;  // ip_output.c:962-963
+    }
+    if (live) out[q] = (uint16_t)res;
+  }
+}
+
 }  // namespace
+
+int launch_spans_lane(const void* base, const uint64_t* off, const uint32_t* len,
+                      const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                      uint32_t flags, bool strided, uint64_t stride, uint32_t slen, int blocks_cu,
+                      hipStream_t stream) {
+  uint64_t blocks = ((uint64_t)n + kBlock - 1) / kBlock;
+  blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, 256ull * (uint64_t)blocks_cu));
+  const dim3 grid((uint32_t)blocks), blk(kBlock);
+  const uint8_t* b = static_cast<const uint8_t*>(base);
+#define UINET_LANE(P, SD, ST)                                                                  \
+  hipLaunchKernelGGL((k_spans_lane<P, SD, ST>), grid, blk, 0, stream, b, off, len, seed, parity, \
+                     out, n, flags, stride, slen)
+  if (strided) {
+    if (seed) UINET_LANE(false, true, true);
+    else UINET_LANE(false, false, true);
+  } else if (parity) {
+    if (seed) UINET_LANE(true, true, false);
+    else UINET_LANE(true, false, false);
+  } else {
+    if (seed) UINET_LANE(false, true, false);
+    else UINET_LANE(false, false, false);
+  }
+#undef UINET_LANE
+  return check_launch();
+}
 
 int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,

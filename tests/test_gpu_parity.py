@@ -206,11 +206,21 @@ def test_spans_far_apart(torch_dev, ora, pipe):
         torch.cuda.empty_cache()
 
 
-def test_spans_small_packets(torch_dev, ora):
-    """The small-packet geometries (4, 8 and 16 lanes per packet): ragged
+@pytest.mark.parametrize("pipe", [1, 3])
+def test_spans_small_packets(torch_dev, ora, pipe):
+    """The small-packet geometries (4, 8 and 16 lanes per packet; with
+    spans_pipe=3 the 4-lane shapes run the lane-per-packet kernel): ragged
     counts, spans longer than the geometry's round, empty spans, seeds,
     parity, UDP; the strided API at 64-B packets, 16-B aligned and not."""
     torch = torch_dev
+    u.set_tuning("spans_pipe", pipe)
+    try:
+        _small_packets(torch, ora)
+    finally:
+        u.set_tuning("spans_pipe", 1)
+
+
+def _small_packets(torch, ora):
     rng = np.random.default_rng(1300)
     arena = rand_arena(24 << 20, 45)
     d_arena = dev(torch, arena)
