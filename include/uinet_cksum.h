@@ -141,31 +141,26 @@ int uinet_cksum_device_ok(void);
 
 /* Performance knobs (process-wide; they never change results):
  *   "blocks_per_cu"   grid-stride launch width, 0 = per-kernel default
- *   "chains_variant"  0 = pipelined chunk stream (default), 1 = serial walk,
- *                     2 = chunk stream with a bitmap segment lookup
- *   "chains_pass"     passes per batch in the chain kernel: 2, 4 (3 with
- *                     chains_variant 2 only; otherwise 2)
+ *   "chains_pass"     64-chunk passes per pipelined batch in the chain
+ *                     kernel: 2 (default) or 4
  *   "chains_long"     chain segments of at least this many 16-B chunks are
  *                     streamed wave-wide; 0 = never, else >= 16 (default 128)
  *   "chains_tile"     packets per wave in the chain kernel: 0 = auto, 8, 32
  *   "xcd_remap"       span kernels: give each XCD a contiguous band of
  *                     packets (1, default) or plain block order (0)
- *   "spans_lut"       span kernels: LDS mask table + one's-complement chunk
- *                     sums (1, default) or register masks + 64-bit sums (0)
  *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
  *                     1..64 (default min(16, hardware threads))
- *   "spans_contig"    span kernels: each block folds one contiguous packet
- *                     range (1) instead of grid-wide rounds (0, default)
- *   "spans_sdesc"     span kernels with 32 or 64 lanes per packet: load the
- *                     wave's packet descriptors with scalar loads (1, default)
- *                     or one vector load per lane group (0)
- *   "spans_pipe"      scalar-descriptor span kernels: lane groups that walk
- *                     4+ packets each (128 blocks per CU) with two in flight
- *                     (1, default), one packet per group (0: 512 blocks per
- *                     CU; ~5 % faster warm, up to 25 % slower in the first
- *                     launches after an idle gap), or one wave per packet
- *                     with scalar per-packet arithmetic (2); the strided
- *                     API at 32 / 64 lanes per packet follows 1 and 0
+ *   "spans_sdesc"     one-shot span kernel (spans_pipe 0) with 32 or 64 lanes
+ *                     per packet: the wave's packet descriptors by scalar
+ *                     loads (1, default) or one vector load per lane group (0)
+ *   "spans_pipe"      span kernel family (span and strided APIs):
+ *                     1 (default) persistent waves with mask-free whole
+ *                     chunks and the per-packet work shared across the wave
+ *                     (k_spans_lean at 32 / 64 lanes per packet, k_spans_quad
+ *                     at 4); 2 = round 2's two-in-flight lane groups at 32 /
+ *                     64 lanes (k_spans_pp; ~1-2 % faster warm, slower under
+ *                     the platform's power ramp); 0 = one packet per lane
+ *                     group, one-shot grid
  *   "spans_geo"       span kernels: force the lanes-per-packet G and loads
  *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
  *                     16x3, 32x3, 64x2, 64x3); 0 = picked from len_hint
@@ -174,16 +169,17 @@ int uinet_cksum_device_ok(void);
  *                     16 chains in lockstep (never changes results)
  *   "host_group"      zero-copy host-mbuf batches: chunks per host thread in
  *                     one pipeline group (1..64, default 1)
+ *   "host_pin"        host pool helpers pinned to CPUs of the process mask
+ *                     (1) or floating (0, default)
  *   "multi_gather"    uinet_cksum_spans_multi: 0 = one RCCL gather when it
  *                     applies (default), 1 = always peer copies
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
- * The environment variables UINET_CKSUM_BLOCKS_PER_CU, UINET_CKSUM_CHAINS
- * (0|1|2, or serial), UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG,
- * UINET_CKSUM_CHAINS_TILE, UINET_CKSUM_XCD_REMAP, UINET_CKSUM_SPANS_LUT,
- * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF, UINET_CKSUM_SPANS_CONTIG,
- * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_SDESC, UINET_CKSUM_SPANS_PIPE and
- * UINET_CKSUM_HOST_GROUP set
- * the initial values. */
+ * The environment variables UINET_CKSUM_BLOCKS_PER_CU,
+ * UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG, UINET_CKSUM_CHAINS_TILE,
+ * UINET_CKSUM_XCD_REMAP, UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF,
+ * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_SDESC, UINET_CKSUM_SPANS_PIPE,
+ * UINET_CKSUM_HOST_GROUP, UINET_CKSUM_HOST_PIN and UINET_CKSUM_MULTI_GATHER
+ * set the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
 /* ------------------------------------------------------------------------ */

@@ -56,10 +56,9 @@ int check_launch() { return record_hip(hipGetLastError()); }
 // launch, so each knob is a relaxed atomic and a launch reads one snapshot
 // (tuning()).  The environment seeds them through the same validation.
 struct TuningLive {
-  std::atomic<int> blocks_per_cu{0}, chains_variant{0}, chains_pass{2}, host_threads{8},
-      chains_long{128}, chains_tile{0}, xcd_remap{1}, spans_lut{1}, walk_prefetch{1},
-      spans_contig{0}, spans_geo{0}, spans_sdesc{1}, spans_pipe{1}, host_group{1}, host_pin{0},
-      multi_gather{0};
+  std::atomic<int> blocks_per_cu{0}, chains_pass{2}, host_threads{8}, chains_long{128},
+      chains_tile{0}, xcd_remap{1}, walk_prefetch{1}, spans_geo{0}, spans_sdesc{1},
+      spans_pipe{1}, host_group{1}, host_pin{0}, multi_gather{0};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -70,19 +69,16 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
   };
   static const Knob knobs[] = {
       {"blocks_per_cu", &TuningLive::blocks_per_cu, [](int v) { return v >= 0 && v <= 4096; }},
-      {"chains_variant", &TuningLive::chains_variant, [](int v) { return v >= 0 && v <= 3; }},
-      {"chains_pass", &TuningLive::chains_pass, [](int v) { return v >= 2 && v <= 4; }},
+      {"chains_pass", &TuningLive::chains_pass, [](int v) { return v == 2 || v == 4; }},
       {"chains_long", &TuningLive::chains_long,
        [](int v) { return v == 0 || (v >= 16 && v <= (1 << 24)); }},
       {"chains_tile", &TuningLive::chains_tile,
        [](int v) { return v == 0 || v == 8 || v == 32; }},
       {"xcd_remap", &TuningLive::xcd_remap, [](int v) { return v == 0 || v == 1; }},
-      {"spans_lut", &TuningLive::spans_lut, [](int v) { return v == 0 || v == 1; }},
       {"host_threads", &TuningLive::host_threads, [](int v) { return v >= 1 && v <= 64; }},
-      {"spans_contig", &TuningLive::spans_contig, [](int v) { return v == 0 || v == 1; }},
       {"spans_geo", &TuningLive::spans_geo, [](int v) { return v == 0 || span_geometry_ok(v); }},
       {"spans_sdesc", &TuningLive::spans_sdesc, [](int v) { return v == 0 || v == 1; }},
-      {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v >= 0 && v <= 3; }},
+      {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v >= 0 && v <= 2; }},
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
       {"host_group", &TuningLive::host_group, [](int v) { return v >= 1 && v <= 64; }},
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
@@ -99,12 +95,11 @@ static TuningLive& tuning_live() {
     const unsigned hw = std::thread::hardware_concurrency();
     x->host_threads = (int)std::min(16u, hw ? hw : 1u);
     static const char* const env[][2] = {
-        {"UINET_CKSUM_BLOCKS_PER_CU", "blocks_per_cu"}, {"UINET_CKSUM_CHAINS", "chains_variant"},
-        {"UINET_CKSUM_CHAINS_PASS", "chains_pass"},     {"UINET_CKSUM_CHAINS_LONG", "chains_long"},
-        {"UINET_CKSUM_CHAINS_TILE", "chains_tile"},     {"UINET_CKSUM_XCD_REMAP", "xcd_remap"},
-        {"UINET_CKSUM_SPANS_LUT", "spans_lut"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
-        {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_CONTIG", "spans_contig"},
-        {"UINET_CKSUM_SPANS_GEO", "spans_geo"},         {"UINET_CKSUM_SPANS_SDESC", "spans_sdesc"},
+        {"UINET_CKSUM_BLOCKS_PER_CU", "blocks_per_cu"}, {"UINET_CKSUM_CHAINS_PASS", "chains_pass"},
+        {"UINET_CKSUM_CHAINS_LONG", "chains_long"},     {"UINET_CKSUM_CHAINS_TILE", "chains_tile"},
+        {"UINET_CKSUM_XCD_REMAP", "xcd_remap"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
+        {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_GEO", "spans_geo"},
+        {"UINET_CKSUM_SPANS_SDESC", "spans_sdesc"},
         {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},       {"UINET_CKSUM_HOST_GROUP", "host_group"},
         {"UINET_CKSUM_HOST_PIN", "host_pin"},          {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},
     };
@@ -112,9 +107,7 @@ static TuningLive& tuning_live() {
       const char* e = getenv(kv[0]);
       if (!e || !*e) continue;
       int v = atoi(e);
-      if (!strcmp(kv[1], "chains_variant") && e[0] == 's') v = 1;  // "serial"
-      if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_lut") ||
-          !strcmp(kv[1], "spans_contig") || !strcmp(kv[1], "spans_sdesc"))
+      if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_sdesc"))
         v = v ? 1 : 0;
       if (std::atomic<int>* f = tuning_field(*x, kv[1], v)) f->store(v, std::memory_order_relaxed);
     }
@@ -128,15 +121,12 @@ Tuning tuning() {
   const auto ld = [](const std::atomic<int>& a) { return a.load(std::memory_order_relaxed); };
   Tuning x;
   x.blocks_per_cu = ld(t.blocks_per_cu);
-  x.chains_variant = ld(t.chains_variant);
   x.chains_pass = ld(t.chains_pass);
   x.host_threads = ld(t.host_threads);
   x.chains_long = ld(t.chains_long);
   x.chains_tile = ld(t.chains_tile);
   x.xcd_remap = ld(t.xcd_remap);
-  x.spans_lut = ld(t.spans_lut);
   x.walk_prefetch = ld(t.walk_prefetch);
-  x.spans_contig = ld(t.spans_contig);
   x.spans_geo = ld(t.spans_geo);
   x.spans_sdesc = ld(t.spans_sdesc);
   x.spans_pipe = ld(t.spans_pipe);

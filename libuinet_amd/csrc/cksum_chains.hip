@@ -30,8 +30,11 @@
 //   * software pipelining: each batch is issued one step before it is summed.
 // Tiles of 8 packets instead of 32 when the batch is small enough that 32
 // would leave too few waves to balance 256 CUs (e.g. jumbo frames).
-// k_chains (UINET_CKSUM_CHAINS=serial, kept for A/B) -- G lanes walk one
-// packet's segments one after another.
+// Formulations measured and removed (code under profiles/r03/pruned/): a
+// serial walk (G lanes per packet, one segment after another), a bitmap
+// segment lookup (chains_variant 2), and k_chains_lean (LDS segment records,
+// bitmap lookup, copy-free two-batch pipeline at 8 waves per SIMD: 40 %
+// slower on config 3, profiles/r03/r03e/ab_c3.log).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -43,50 +46,12 @@
 namespace uinet {
 namespace {
 
-template <int G, int U, typename OffT, typename LenT>
-__global__ __launch_bounds__(kBlock) void k_chains(const uint8_t* __restrict__ base,
-                                                  const OffT* __restrict__ seg_off,
-                                                  const LenT* __restrict__ seg_len,
-                                                  const uint32_t* __restrict__ pkt_seg,
-                                                  const uint32_t* __restrict__ plen,
-                                                  const uint32_t* __restrict__ pskip,
-                                                  const uint32_t* __restrict__ seed,
-                                                  uint16_t* __restrict__ out, uint32_t n,
-                                                  uint32_t flags) {
-  constexpr uint32_t kGroups = kBlock / G;
-  const int gl = threadIdx.x & (G - 1);
-  const uint32_t stride = gridDim.x * kGroups;
-  for (uint32_t p = blockIdx.x * kGroups + threadIdx.x / G; p < n; p += stride) {
-    const uint32_t s0 = pkt_seg[p], s1 = pkt_seg[p + 1];
-    const uint32_t lo_want = pskip ? pskip[p] : 0u;
-    const uint32_t hi_want = plen ? plen[p] : 0xffffffffu;
-    uint64_t tot = 0;
-    uint32_t pos = 0;  // chain offset of segment s
-    for (uint32_t s = s0; s < s1 && pos < hi_want; ++s) {
-      const uint32_t l = (uint32_t)seg_len[s];
-      const uint32_t lo = lo_want > pos ? min(lo_want - pos, l) : 0u;
-      const uint32_t hi = min(hi_want - pos, l);
-      if (hi > lo) {
-        const uint8_t* a = base + (uint64_t)seg_off[s] + lo;
-        uint32_t x = fold16(span_lane_sum<G, U>(a, hi - lo, gl));
-        const uint32_t lpar = pos + lo - lo_want;  // logical offset of a
-        if ((lpar ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
-        tot += x;
-      }
-      pos += l;
-    }
-    const uint32_t x = group_sum<G>(fold16(tot));
-    if (gl == 0) out[p] = finish((uint64_t)x + (seed ? seed[p] : 0u), flags);
-  }
-}
-
 constexpr int kWaves = kBlock / 64;
 #ifndef UINET_CHAINS_LONGU  // build-time A/B knob (profiles/r01/ab/chains_occ/longu)
 #define UINET_CHAINS_LONGU 4
 #endif
 constexpr int kLongU = UINET_CHAINS_LONGU;  // chunks in flight per lane on a long segment
 constexpr uint32_t kListMax = 1024;  // longest segment (chunks) the chunk list takes
-constexpr uint32_t kListMaxBm = 128;  // the same for the bitmap lookup (<= 127 words)
 
 // 16-B raw buffer load, non-temporal (aux bit 1), from a resource spanning
 // 4 GiB: one VGPR of offset instead of a 64-bit address per chunk.
@@ -133,7 +98,7 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 #define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(kPass == 2 ? 6 : 1)))
 #endif
 
-template <int kPass, int kTile, bool kBm, typename OffT, typename LenT>
+template <int kPass, int kTile, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
                                                        const LenT* __restrict__ seg_len,
@@ -150,24 +115,16 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
   __shared__ MaskLut lut;
   __shared__ unsigned long long lds_acc[kWaves][2 * kTile];  // (slot, rot) bins
   __shared__ uint32_t lds_pkmark[kWaves][64];  // packet-start markers (slot + 1)
-  // kBm = false: segment-start markers (lane + 1) per batch;
-  // kBm = true: the round's segment starts as a bitmap over its chunk list
-  // (bit c of word c / 64), at most 64 * (kListMaxBm - 1) chunks
-  constexpr int kMarkB = kBm ? 1 : kWin;
-  constexpr int kBmWords = kBm ? (int)kListMaxBm : 1;
-  __shared__ uint8_t lds_mark[kWaves][kMarkB];
-  __shared__ unsigned long long lds_bm[kWaves][kBmWords];
+  __shared__ uint8_t lds_mark[kWaves][kWin];  // segment-start markers (lane + 1) per batch
   lut.init();
   for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
-  for (int i = threadIdx.x; i < kWaves * kMarkB; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
-  for (int i = threadIdx.x; i < kWaves * kBmWords; i += blockDim.x) (&lds_bm[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kWaves * kWin; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   unsigned long long* acc = lds_acc[wid];
   uint32_t* pkmark = lds_pkmark[wid];
   uint8_t* mark = lds_mark[wid];
-  unsigned long long* bm = lds_bm[wid];
   const uint32_t tiles = (n + kTile - 1) / kTile;
   const uint32_t wstride = gridDim.x * kWaves;
 
@@ -265,7 +222,7 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
       // --- long segments: one wave-wide span each -------------------------
       const bool is_long =
-          nch >= (kBm ? kListMaxBm : kListMax) || (long_ch != 0 && nch >= long_ch);
+          nch >= kListMax || (long_ch != 0 && nch >= long_ch);
       for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
         const int s = (int)__builtin_ctzll(lm);
         // head and length read separately: a segment may hold up to 4 GiB,
@@ -316,75 +273,9 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint32_t dkr = (uint32_t)rel - 16u * cst;  // mod 2^32; + 16 c lands in range
       const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(base + (R0 - (1ull << 31)));
       uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the batch
-      // kBm: the list segments' records compacted to lanes 0..L-1 in list
-      // order (ds_permute; the other lanes park theirs in L..63), the bitmap
-      // of their start chunks built by LDS atomics, 64 of its words held one
-      // per lane.  A chunk's segment is then the number of starts at or
-      // before it: two readlanes and an mbcnt per pass, no LDS round trip.
-      uint32_t cA = recA, cB = recB, cD0 = 0, cD1 = 0;
-      uint64_t bmw = 0;
-      uint32_t segc = 0;  // list segments started before the batch
-      if constexpr (kBm) {
-        if (nch_l != 0) atomicOr(&bm[cst >> 6], 1ull << (cst & 63u));
-        const uint32_t lrank = __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(lm_list >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm_list, 0u));
-        const int dst = 4 * (nch_l != 0 ? (int)lrank : 63 - (lane - (int)lrank));
-        cA = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)recA);
-        cB = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)recB);
-        if (window) {
-          cD0 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)dkr);
-        } else {
-          cD0 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)dk);
-          cD1 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(dk >> 32));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        bmw = bm[lane];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        bm[lane] = 0;
-      }
       // Issue the batch at list chunk b into (v, key): segment lookup, mask
       // index and bin, loads.  Nothing here waits for packet bytes.
       auto issue = [&](uint32_t b, u32x4 (&v)[kPass], uint32_t (&key)[kPass], auto kWindow) {
-        if constexpr (kBm) {
-          if (b != 0 && (b & 4095u) == 0) {  // words 64..: lists of more than 4096 chunks
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            bmw = bm[(b >> 6) + (uint32_t)lane];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            bm[(b >> 6) + (uint32_t)lane] = 0;
-          }
-#pragma unroll
-          for (int q = 0; q < kPass; ++q) {
-            const int j = (int)(((b >> 6) + (uint32_t)q) & 63u);
-            const uint64_t M =
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bmw >> 32), j) << 32) |
-                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bmw, j);
-            // starts at or before the lane's chunk: bit 0, plus the bits of
-            // M >> 1 below the lane (mbcnt counts the bits below the lane)
-            const uint64_t Mr = M >> 1;
-            const int seg = (int)__builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(Mr >> 32),
-                __builtin_amdgcn_mbcnt_lo((uint32_t)Mr, segc + (uint32_t)(M & 1u) - 1u));
-            segc += (uint32_t)__builtin_popcountll(M);
-            const uint32_t c = b + (uint32_t)(q * 64 + lane);
-            const bool in = c < C;
-            const uint32_t cc = in ? c : C - 1;
-            const uint32_t a = (uint32_t)__shfl(cA, seg);
-            const uint32_t bq = (uint32_t)__shfl(cB, seg);
-            const int base16 = 16 * (int)c;
-            const int s_lo = (int)(a & 0xfffffu) - base16;
-            const int s_hi = in ? (int)bq - base16 : s_lo;
-            key[q] = MaskLut::index(s_lo, s_hi) | ((a >> 20) << 16);
-            if constexpr (decltype(kWindow)::value) {
-              const uint32_t d = (uint32_t)__shfl(cD0, seg);
-              v[q] = load_chunk_buf(rsrc, d + 16u * cc);
-            } else {
-              const uint32_t lo32 = (uint32_t)__shfl(cD0, seg);
-              const uint32_t hi32 = (uint32_t)__shfl(cD1, seg);
-              v[q] = load_chunk(base + ((((uint64_t)hi32 << 32) | lo32) + 16ull * cc));
-            }
-          }
-          return;
-        }
         const bool mk = nch_l != 0 && cst >= b && cst < b + kWin;
         if (mk) mark[cst - b] = (uint8_t)(lane + 1);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -457,52 +348,15 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
 #endif
 }
 
-struct Geometry {
-  int g, u;
-};
-
-Geometry pick_serial(uint32_t mean_seg) {
-  if (mean_seg == 0) return {64, 2};
-  if (mean_seg <= 96) return {8, 1};
-  if (mean_seg <= 224) return {8, 2};
-  if (mean_seg <= 720) return {16, 3};
-  if (mean_seg <= 1520) return {32, 3};
-  return {64, 3};
-}
-
-}  // namespace
-
-namespace {
-
 template <typename OffT, typename LenT>
 int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
                     const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                     const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
                     uint32_t len_hint, hipStream_t stream) {
+  (void)len_hint;  // the chunk stream does not depend on segment lengths
   if (n == 0) return UINET_CKSUM_OK;
   const Tuning& tn = tuning();
   const uint8_t* b = static_cast<const uint8_t*>(base);
-  if (tn.chains_variant == 1) {
-    // len_hint = mean SEGMENT length: the group walks one segment at a time
-    const Geometry geo = pick_serial(len_hint);
-    const uint32_t gpb = kBlock / geo.g;
-    uint64_t blocks = ((uint64_t)n + gpb - 1) / gpb;
-    const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
-    blocks = blocks > cap ? cap : blocks;
-#define L(G, U)                                                                              \
-  hipLaunchKernelGGL((k_chains<G, U, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, b, seg_off, \
-                     seg_len, pkt_seg, len, skip, seed, out, n, flags)
-    switch (geo.g * 16 + geo.u) {
-      case 8 * 16 + 1: L(8, 1); break;
-      case 8 * 16 + 2: L(8, 2); break;
-      case 16 * 16 + 3: L(16, 3); break;
-      case 32 * 16 + 3: L(32, 3); break;
-      case 64 * 16 + 2: L(64, 2); break;
-      default: L(64, 3); break;
-    }
-#undef L
-    return check_launch();
-  }
   // Tile of 32 packets, or 8 when 32 would give fewer than 16 tiles per CU
   // (5tso, 131 K packets, runs 0.8 % faster at 32: profiles/r01/ab/bpc_s6/tile).
   const int tile = tn.chains_tile ? tn.chains_tile : (n >= 32u * 4096u ? 32 : 8);
@@ -511,31 +365,15 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
-  if (tn.chains_variant == 3)
-    return launch_chains_lean_t(base, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags,
-                                tile, blocks_per_cu(64), long_ch, stream);
-#define LF(P, T, BM)                                                                          \
-  hipLaunchKernelGGL((k_chains_pipe<P, T, BM, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, \
-                     b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
-  const bool bmv = tn.chains_variant == 2;
+#define LF(P, T)                                                                           \
+  hipLaunchKernelGGL((k_chains_pipe<P, T, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0,   \
+                     stream, b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
   if (tile == 8) {
-    if (tn.chains_pass == 4)
-      LF(4, 8, false);
-    else if (bmv)
-      LF(2, 8, true);
-    else
-      LF(2, 8, false);
+    if (tn.chains_pass == 4) LF(4, 8);
+    else LF(2, 8);
   } else {
-    if (bmv && tn.chains_pass == 3)
-      LF(3, 32, true);
-    else if (bmv && tn.chains_pass == 4)
-      LF(4, 32, true);
-    else if (tn.chains_pass == 4)
-      LF(4, 32, false);
-    else if (bmv)
-      LF(2, 32, true);
-    else
-      LF(2, 32, false);
+    if (tn.chains_pass == 4) LF(4, 32);
+    else LF(2, 32);
   }
 #undef LF
   return check_launch();

@@ -14,18 +14,15 @@ namespace uinet {
 // a snapshot of the live values (relaxed atomics in cksum_api.hip).
 struct Tuning {
   int blocks_per_cu;   // grid-stride width
-  int chains_variant;  // 0 pipelined chunk stream, 1 serial walk
-  int chains_pass;     // 2, 4
+  int chains_pass;     // flat chains: 64-chunk passes per pipelined batch, 2 or 4
   int host_threads;    // host-mbuf batch walk/pack threads, 1..64
   int chains_long;     // flat chains: segments of >= this many 16-B chunks stream
                        // wave-wide (0 = never)
   int chains_tile;     // flat chains: packets per wave tile, 0 = auto, 8, 32
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
-  int spans_lut;       // span kernels: LDS mask table + one's-complement sums (0/1)
-  int spans_contig;    // span kernels: block-contiguous packet ranges (0/1)
   int spans_sdesc;     // span kernels: per-wave scalar descriptor loads (0/1)
-  int spans_pipe;      // scalar-descriptor span kernels: persistent groups with two
-                       // packets in flight (k_spans_pp, 128 blocks per CU) (0/1)
+  int spans_pipe;      // span kernel family: 1 k_spans_lean / k_spans_quad (persistent,
+                       // mask-free whole chunks), 2 k_spans_pp, 0 one-shot k_spans
   int spans_geo;       // span kernels: lanes-per-packet G and loads-per-lane U
                        // as G * 16 + U (0 = picked from the mean length)
   int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead, 2 lockstep chase
@@ -54,17 +51,12 @@ int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream);
-// k_chains_lean (cksum_chains_lean.hip): tile 8 or 32 packets per wave.
-template <typename OffT, typename LenT>
-int launch_chains_lean_t(const void* base, const OffT* seg_off, const LenT* seg_len,
-                         const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
-                         const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
-                         int tile, int bpc, uint32_t long_ch, hipStream_t stream);
-// k_spans_lane (cksum_spans.hip): one lane per packet, for small packets.
-int launch_spans_lane(const void* base, const uint64_t* off, const uint32_t* len,
+// k_spans_quad (cksum_spans.hip): 4 lanes per packet, U = 1 or 2 chunk
+// slots per lane, for small packets.
+int launch_spans_quad(const void* base, const uint64_t* off, const uint32_t* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
-                      uint32_t flags, bool strided, uint64_t stride, uint32_t slen, int blocks_cu,
-                      hipStream_t stream);
+                      uint32_t flags, int u, bool strided, uint64_t stride, uint32_t slen,
+                      int blocks_cu, hipStream_t stream);
 int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
                   const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                   const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,

@@ -86,7 +86,7 @@ __device__ __forceinline__ uint32_t wave_u32(const uint32_t* __restrict__ a, uin
   return r;
 }
 
-template <int G, int U, bool kStrided, bool kLut, bool kSDesc = false>
+template <int G, int U, bool kStrided, bool kSDesc = false>
 __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ base,
                                                  const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ len,
@@ -94,26 +94,16 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
                                                  const uint8_t* __restrict__ parity,
                                                  uint64_t pkt_stride, uint32_t fixed_len,
                                                  uint16_t* __restrict__ out, uint32_t n,
-                                                 uint32_t flags, uint32_t remap,
-                                                 uint32_t contig) {
+                                                 uint32_t flags, uint32_t remap) {
   constexpr uint32_t kGroups = kBlock / G;
   __shared__ MaskLut lut;
   const int gl = threadIdx.x & (G - 1);
-  // contig = 0: round r of the grid covers packets [r S, (r + 1) S), S = the
-  // grid's group count (a group's packets lie S apart).  contig = 1: block b
-  // owns the contiguous range [b C, (b + 1) C), C = kGroups * ceil(n / S),
-  // and its groups step through it kGroups apart.  Interleaved A/B on one box
-  // (profiles/r01/ab/contig/): config 2 -1.1 %, 2rx -1.0 %, 5 equal, 64-B
-  // packets +1.1 %; the default stays 0.
+  // round r of the grid covers packets [r S, (r + 1) S), S = the grid's
+  // group count (a group's packets lie S apart)
   const uint32_t S = gridDim.x * kGroups;
-  const uint32_t lb = logical_block(remap);
-  uint32_t stride = S, p = lb * kGroups + threadIdx.x / G, pend = n;
-  if (contig) {
-    const uint32_t chunk = ((n + S - 1) / S) * kGroups;
-    stride = kGroups;
-    p = lb * chunk + threadIdx.x / G;
-    pend = min(n, lb * chunk + chunk);
-  }
+  const uint32_t stride = S;
+  uint32_t p = logical_block(remap) * kGroups + threadIdx.x / G;
+  const uint32_t pend = n;
   const bool live = p < pend;
   uint64_t o = 0;
   uint32_t l = 0;
@@ -128,7 +118,7 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
   Span<G, U> sp;
   sp.init(a, l);
   if (l) sp.load(0, gl);  // the first packet's bytes are in flight ...
-  if (kLut) lut.init();   // ... while the block fills its mask table (every thread
+  lut.init();             // ... while the block fills its mask table (every thread
                           // reaches this barrier: no exit before it)
   if (!live) return;      // whole groups leave together
   for (;;) {
@@ -143,16 +133,10 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
       on = kStrided ? (uint64_t)pc * pkt_stride : off[pc];
       ln = kStrided ? fixed_len : len[pc];
     }
-    uint32_t x;
-    if (kLut) {
-      // a span of one round folds its 32-bit sum (< U * 2^19) directly
-      const uint32_t a0 = l ? sp.sum_lut_first(lut, gl) : 0u;
-      x = sp.nch > (uint32_t)(G * U) ? fold16((uint64_t)a0 + sp.rest_lut(lut, gl)) : fold16_32(a0);
-    } else {
-      uint64_t acc = l ? sp.sum(0, gl) : 0;
-      if (sp.nch > (uint32_t)(G * U)) acc += sp.rest(gl);
-      x = fold16(acc);
-    }
+    // a span of one round folds its 32-bit sum (< U * 2^19) directly
+    const uint32_t a0 = l ? sp.sum_lut_first(lut, gl) : 0u;
+    uint32_t x =
+        sp.nch > (uint32_t)(G * U) ? fold16((uint64_t)a0 + sp.rest_lut(lut, gl)) : fold16_32(a0);
     const uint32_t lp = parity ? parity[p] : 0u;
     if ((lp ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1) x = rot8(x);
     x = group_sum<G>(x);
@@ -284,117 +268,6 @@ __global__ __launch_bounds__(kBlock) void k_spans_pp(const uint8_t* __restrict__
   }
 }
 
-// k_spans_w: one wave per packet, two packets in flight per wave, and every
-// per-packet quantity wave-uniform.  A packet's offset, length, seed and
-// chunk geometry are scalar loads and SALU arithmetic; its U * 64 chunk loads
-// take the scalar base plus a 32-bit lane offset; the 64 lane sums meet in a
-// DPP scan and the fold, rotation and complement run on the scalar unit.
-// About 36 VALU instructions per KiB (ISA count) against 47 for k_spans_pp and ~66 for the
-// one-packet-per-group grid: under the power ramp of a burst the clock
-// holds (a streaming read with 64 integer multiply-adds per 16-B chunk dips
-// like the one-shot grid, one with 32 does not: profiles/r02/cold_ab/).
-template <int U, bool kParity>
-__global__ __launch_bounds__(kBlock) void k_spans_w(const uint8_t* __restrict__ base,
-                                                   const uint64_t* __restrict__ off,
-                                                   const uint32_t* __restrict__ len,
-                                                   const uint32_t* __restrict__ seed,
-                                                   const uint8_t* __restrict__ parity,
-                                                   uint16_t* __restrict__ out, uint32_t n,
-                                                   uint32_t flags, uint32_t remap) {
-  constexpr int kChunks = 64 * U;
-  __shared__ MaskLut lut;
-  const int lane = threadIdx.x & 63;
-  constexpr uint32_t kWavesPB = kBlock / 64;
-  const uint32_t W = gridDim.x * kWavesPB;  // packets per round of the grid
-  const uint32_t p0 =
-      __builtin_amdgcn_readfirstlane(logical_block(remap) * kWavesPB + (threadIdx.x >> 6));
-  struct Desc {
-    const uint8_t* c0;  // first aligned chunk (the arena start for an empty span)
-    int head, end;      // the span is bytes [head, end) from c0
-    uint32_t last;      // its last chunk
-    uint32_t sd;        // seed
-    uint32_t lp;        // logical parity (a vector load, one packet ahead)
-    uint32_t odd;       // address parity of the span's first byte
-  };
-  auto desc = [&](uint32_t q) {
-    Desc d;
-    const uint32_t qc = min(q, n - 1);
-    const uint64_t o = sload64(off + qc);
-    const uint32_t l = q < n ? sload32(len + qc) : 0u;
-    const uint8_t* a = base + o;
-    d.head = l ? (int)(reinterpret_cast<uintptr_t>(a) & 15) : 0;
-    d.c0 = l ? a - d.head : base;
-    d.end = d.head + (int)l;
-    d.last = l ? ((uint32_t)(d.end + 15) >> 4) - 1u : 0u;
-    d.sd = seed ? sload32(seed + qc) : 0u;
-    d.lp = kParity ? parity[qc] : 0u;
-    d.odd = (uint32_t)reinterpret_cast<uintptr_t>(a) & 1u;
-    return d;
-  };
-  auto load = [&](const Desc& d, u32x4 (&v)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = load_chunk(d.c0 + 16u * min((uint32_t)(u * 64 + lane), d.last));
-  };
-  uint32_t res = 0, slot = 0;  // lane j: the result of packet p0 + j * W
-  auto done = [&](const Desc& d, const u32x4 (&v)[U]) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int b = 16 * (u * 64 + lane);
-      acc += lut.sum_oc(v[u], d.head - b, d.end - b);
-    }
-    uint64_t s64 = fold16_32(acc);
-    if (d.end > 16 * kChunks) {  // longer than one round: the rest as in k_spans
-      for (uint32_t k0 = kChunks; k0 <= d.last; k0 += kChunks) {
-        u32x4 w[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          w[u] = load_chunk(d.c0 + 16u * min(k0 + (uint32_t)(u * 64 + lane), d.last));
-        uint32_t r = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int b = 16 * (int)(k0 + (uint32_t)(u * 64 + lane));
-          r += lut.sum_oc(w[u], d.head - b, d.end - b);
-        }
-        s64 += fold16_32(r);
-      }
-    }
-    // the wave's total, then the scalar unit's fold / rotation / complement
-    const uint32_t tot =
-        __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(s64), 0u), 63);  // < 2^22
-    uint32_t x = fold16_32(tot);
-    if ((d.lp ^ d.odd) & 1) x = rot8(x);
-    // results wait in lane `slot` of `res` and are stored after the loop (the
-    // host sizes the grid so that no wave folds more than 64 packets): a
-    // store inside the loop makes the next packet's loads wait for it
-    if (lane == (int)slot) res = finish((uint64_t)x + d.sd, flags);
-    ++slot;
-  };
-  u32x4 vA[U], vB[U];
-  Desc dA = desc(p0);
-  load(dA, vA);
-  lut.init();  // every thread reaches this barrier: no exit before it
-  if (p0 >= n) return;  // wave-uniform
-  uint32_t p = p0;
-  Desc dB = desc(p + W);
-  for (;;) {
-    load(dB, vB);  // packet p + W in flight while p is folded
-    const Desc dC = desc(p + 2 * W);
-    done(dA, vA);
-    if (p + W >= n) break;
-    load(dC, vA);  // packet p + 2W in flight while p + W is folded
-    const Desc dD = desc(p + 3 * W);
-    done(dB, vB);
-    if (p + 2 * W >= n) break;
-    p += 2 * W;
-    dA = dC;
-    dB = dD;
-  }
-  const uint32_t q = p0 + (uint32_t)lane * W;
-  if ((uint32_t)lane < slot && q < n) out[q] = (uint16_t)res;
-}
-
 struct Geometry {
   int g, u;
 };
@@ -465,46 +338,37 @@ int blocks_per_cu(int dflt) {
   return v > 0 ? v : dflt;
 }
 
+// spans_pipe selects the span kernel family for G >= 32 (knob "spans_pipe",
+// UINET_CKSUM_SPANS_PIPE):
+//   1 (default) k_spans_lean (cksum_spans.hip): persistent waves, scalar
+//     descriptors, mask-free whole chunks -- 23 VALU instructions per KiB,
+//     no power-ramp dip in the driver's window (profiles/r03/r03d/); at 4
+//     lanes per packet (mean length <= 64 B) k_spans_quad;
+//   2 k_spans_pp: round 2's default, kept for A/B (1-2 % faster warm, 53.7
+//     VALU / KiB, dips to 0.79 of peak late in the driver's window);
+//   0 k_spans: one packet per lane group, one-shot grid.
+// Geometries other than 32 x 3 / 64 x 3 (the spans_geo override) use k_spans_pp
+// under 1 and 2.
 int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
                  const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                  uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = geometry_override(pick_geometry(len_hint));
+  const int pipe = tuning().spans_pipe;
   // Scalar descriptors (G >= 32, knob "spans_sdesc", default on): a wave's
   // 1-2 packets' off / len come from s_loads, and the grid drops to one packet
   // per group (512 blocks per CU at 1 M x 1500 B).  Interleaved A/B, config 2
   // (profiles/r02/ab_sdesc/): vector descriptors at 256 / CU 0.2192 ms,
   // scalar at 256 / CU 0.2167, scalar at 512 / CU 0.2086 (+5.1 %), 4096 / CU
   // 0.2095; on a slower stretch of the same box +1.4 %.
-  if (tuning().spans_pipe == 3 && geo.g == 4)
-    return launch_spans_lane(base, off, len, seed, parity, out, n, flags, false, 0, 0,
+  if (pipe == 1 && geo.g == 4)
+    return launch_spans_quad(base, off, len, seed, parity, out, n, flags, geo.u, false, 0, 0,
                              blocks_per_cu(32), stream);
   const bool sdesc = tuning().spans_sdesc && geo.g >= 32;
-  if (sdesc && tuning().spans_pipe == 3 && geo.u == 3)
+  if (sdesc && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, false, 0, 0,
                              blocks_per_cu(128), stream);
-  if (sdesc && tuning().spans_pipe == 2) {
-    // one wave per packet: U loads per lane cover U * 64 chunks
-    const int u = len_hint <= 2032 ? 2 : 3;
-    // at most 64 packets per wave (its results are stored from one register)
-    const int grid = std::max<int>(grid_for(n, 64, 128), (int)(((uint64_t)n + 255) / 256));
-#define LW(U)                                                                             \
-  if (parity)                                                                             \
-    hipLaunchKernelGGL((k_spans_w<U, true>), dim3(grid), dim3(kBlock), 0, stream,          \
-                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
-                       flags, (uint32_t)tuning().xcd_remap);                               \
-  else                                                                                    \
-    hipLaunchKernelGGL((k_spans_w<U, false>), dim3(grid), dim3(kBlock), 0, stream,         \
-                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
-                       flags, (uint32_t)tuning().xcd_remap)
-    if (u == 2)
-      LW(2);
-    else
-      LW(3);
-#undef LW
-    return check_launch();
-  }
-  if (sdesc && tuning().spans_pipe) {
+  if (sdesc && pipe) {
     const int grid = grid_for(n, geo.g, 128);
 #define LP(G, U)                                                                          \
   if (parity)                                                                             \
@@ -526,20 +390,13 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   const int grid = grid_for(n, geo.g, sdesc ? 512 : 256);
 #define L(G, U)                                                                          \
   if (sdesc && (G) >= 32)                                                                \
-    hipLaunchKernelGGL((k_spans<G, U, false, true, true>), dim3(grid), dim3(kBlock), 0,  \
-                       stream, static_cast<const uint8_t*>(base), off, len, seed, parity, \
-                       0ull, 0u, out, n, flags, (uint32_t)tuning().xcd_remap,            \
-                       (uint32_t)tuning().spans_contig);                                 \
-  else if (tuning().spans_lut)                                                           \
     hipLaunchKernelGGL((k_spans<G, U, false, true>), dim3(grid), dim3(kBlock), 0, stream, \
                        static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
-                       out, n, flags, (uint32_t)tuning().xcd_remap,                      \
-                       (uint32_t)tuning().spans_contig);                                 \
+                       out, n, flags, (uint32_t)tuning().xcd_remap);                     \
   else                                                                                   \
-    hipLaunchKernelGGL((k_spans<G, U, false, false>), dim3(grid), dim3(kBlock), 0, stream, \
+    hipLaunchKernelGGL((k_spans<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,       \
                        static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
-                       out, n, flags, (uint32_t)tuning().xcd_remap,                      \
-                       (uint32_t)tuning().spans_contig)
+                       out, n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
@@ -552,15 +409,14 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   // 16-B aligned packets of at most 64 B hold at most 4 chunks: one per lane
   if (len <= 64 && ((reinterpret_cast<uintptr_t>(base) | pkt_stride) & 15) == 0) geo = {4, 1};
   geo = geometry_override(geo);
-  // one packet per group suits long packets; small ones want groups that
-  // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
-  if (tuning().spans_pipe == 3 && geo.g == 4)
-    return launch_spans_lane(base, nullptr, nullptr, seed, nullptr, out, n, flags, true,
+  const int pipe = tuning().spans_pipe;
+  if (pipe == 1 && geo.g == 4)
+    return launch_spans_quad(base, nullptr, nullptr, seed, nullptr, out, n, flags, geo.u, true,
                              pkt_stride, len, blocks_per_cu(32), stream);
-  if (geo.g >= 32 && tuning().spans_pipe == 3 && geo.u == 3)
+  if (geo.g >= 32 && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, nullptr, nullptr, seed, nullptr, out, n, flags, geo.g, true,
                              pkt_stride, len, blocks_per_cu(128), stream);
-  if (geo.g >= 32 && tuning().spans_pipe == 1) {
+  if (geo.g >= 32 && pipe) {
     // the persistent two-in-flight groups of k_spans_pp, descriptors from
     // the stride: as for the span API, the one-shot grid (spans_pipe = 0)
     // slows under the platform's power limit (profiles/r02/ab_strided_pp/)
@@ -577,18 +433,13 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
 #undef LS
     return check_launch();
   }
+  // one packet per group suits long packets; small ones want groups that
+  // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
   const int grid = grid_for(n, geo.g, len <= 96 ? 256 : 4096);
-#define L(G, U)                                                                         \
-  if (tuning().spans_lut)                                                               \
-    hipLaunchKernelGGL((k_spans<G, U, true, true>), dim3(grid), dim3(kBlock), 0, stream, \
-                       static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
-                       pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap,     \
-                       (uint32_t)tuning().spans_contig);                                 \
-  else                                                                                  \
-    hipLaunchKernelGGL((k_spans<G, U, true, false>), dim3(grid), dim3(kBlock), 0, stream, \
-                       static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
-                       pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap,     \
-                       (uint32_t)tuning().spans_contig)
+#define L(G, U)                                                                        \
+  hipLaunchKernelGGL((k_spans<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,        \
+                     static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
+                     pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();

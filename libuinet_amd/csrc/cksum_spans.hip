@@ -1,5 +1,6 @@
 // k_spans_lean: the span kernel for 32 and 64 lanes per packet (packets of
-// 0.7 KB and up; config 2's 1500 B, config 4, config 5's 9000 B).
+// 0.7 KB and up; config 2's 1500 B, config 4, config 5's 9000 B), and
+// k_spans_quad (below) for 4 lanes per packet (small packets).
 //
 // Same arithmetic as the other span kernels (cksum_device.h; reference
 // /root/reference/sys/amd64/amd64/in_cksum.c:91-170,193-232): every byte at
@@ -418,7 +419,10 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   u32x4 vA[kU], vB[kU];
   Geo<kP> zA = load_step(desc(min(q, qmax)), vA);
   lut.m[threadIdx.x] = lw0;
-  if (threadIdx.x + kBlock < 17u * 17u) lut.m[threadIdx.x + kBlock] = lw1;
+  // unconditional (threads past the table rewrite its last entry with the
+  // same word): under a branch the compiler sinks lw1's load into it and waits
+  // for every load in flight, the first step's chunks included
+  lut.m[min(threadIdx.x + kBlock, 17u * 17u - 1u)] = lw1;
   __syncthreads();  // every thread reaches this barrier: no exit before it
   if (q >= n) return;  // wave-uniform
   const uint32_t K = (n - q + S - 1) / S;  // live steps of this wave, >= 1
@@ -443,132 +447,284 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   }
 }
 
-// k_spans_lane: one LANE per packet, for small packets (<= 64 B; config 2s
-// shapes).  Round 2 found 64-B packets bound by per-packet vector work, not
-// by bytes in flight (profiles/r02/ab_small/): with 4 lanes per packet every
-// packet pays its mask-table sums, a 2-step butterfly, the fold, rotation,
-// complement and store, for 64 bytes.  Here each lane folds its own packet:
-// no cross-lane reduction at all, and every per-packet instruction serves 64
-// packets.  A lane loads its packet's kLU 16-byte chunks (5 hold any span of
-// <= 65 B at any alignment); one load instruction touches 64 packets' chunks
-// (64 x 16 B over 4 KiB; the wave's kLU loads consume every byte of those
-// lines, through L1), its descriptors are one coalesced vector load per array.
-// A chunk slot that no lane needs masked (aligned 64-B packets: all but the
-// last) skips the mask table.  Longer spans (ragged batches) finish with
-// further rounds of kLU chunks.
-constexpr int kLU = 5;
-
-template <bool kParity, bool kSeed, bool kStrided>
-__global__ __launch_bounds__(kBlock) void k_spans_lane(
+// k_spans_quad: 4 lanes per packet, for small packets (mean length <= 64 B:
+// config 2s shapes).  Round 2 found 64-B packets bound by per-packet vector
+// work (~110 VALU instructions per KiB in k_spans<4, 2>, and a wait for all
+// loads in flight once per packet: profiles/r02/ab_small/); one lane per
+// packet (round 3) made every chunk load touch 64 lines and ran 70 % slower
+// (profiles/r03/r03e/ab_span_c2s.log).  Here a wave folds 16 packets per step
+// with the pipeline of k_spans_lean:
+//  * descriptors come per super-step of 64 packets (4 steps): one coalesced
+//    vector load per array, one lane per packet, issued a whole super-step
+//    before its first step; a step's quads take their packet's words with
+//    ds_bpermute.  (Per-step descriptor loads, issued one step ahead, chained
+//    each step's chunk loads to a descriptor round trip: ~1 KiB per wave per
+//    memory latency, 20 % slower than k_spans on config 2s.)
+//  * a lane's U chunk slots are chunks gl, 4 + gl (64-bit addresses, clamped
+//    to the packet's last chunk); a slot that every lane holds whole skips the
+//    mask table, one that every lane holds empty skips the sum (ballots);
+//  * step k + 1's chunks are loaded before step k is summed; no load sits
+//    under a branch in the loop;
+//  * a packet's 4 lane partials meet in 2 DPP quad_perm adds, and the fold,
+//    rotation, seed and complement run branch-free in every lane; lane i
+//    collects packet i's result of the super-step (one ds_bpermute per step)
+//    and the 64 results leave in one 128-B store (through a buffer resource:
+//    lanes past the batch address past its end).
+template <int U, bool kParity, bool kSeed, bool kStrided>
+__global__ __launch_bounds__(kBlock) void k_spans_quad(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed,
     const uint8_t* __restrict__ parity, uint16_t* __restrict__ out, uint32_t n, uint32_t flags,
-    uint64_t stride, uint32_t slen) {
+    uint32_t remap, uint64_t stride, uint32_t slen) {
+  constexpr uint32_t kRoundB = 64u * U;  // bytes of a span one round covers
+  constexpr uint32_t kWavesPB = kBlock / 64;
   __shared__ MaskLut lut;
-  const u32x4* lsrc = reinterpret_cast<const u32x4*>(g_mask_words.w);
-  lut.m[threadIdx.x] = lsrc[threadIdx.x];
-  if (threadIdx.x + kBlock < 17u * 17u) lut.m[threadIdx.x + kBlock] = lsrc[threadIdx.x + kBlock];
-  __syncthreads();  // every thread reaches this barrier: no exit before it
-  const uint32_t boff = (uint32_t)(reinterpret_cast<uintptr_t>(base) & 15);
-  const uint8_t* abase = base - boff;
-  const uint32_t step = gridDim.x * kBlock;
-  // descriptors one iteration ahead, behind the data loads (index clamped to
-  // the batch, so the prefetch is unconditional)
-  auto fetch = [&](uint32_t q, uint64_t& o, uint32_t& l) {
-    const uint32_t qc = min(q, n - 1);
+  const uint32_t lane = threadIdx.x & 63, gi = lane >> 2, gl = lane & 3;
+  const __amdgpu_buffer_rsrc_t out_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(2u * n), 0x00020000);
+
+  // A super-step's raw descriptors, lane i = packet p0 + i (index clamped to
+  // the batch: loads only, no branch).
+  struct B {
+    uint32_t olo, ohi, l, sd, lp;
+  };
+  auto blk = [&](uint32_t p0) {
+    B d{};
+    if constexpr (!kStrided) {
+      const uint32_t qc = min(p0 + lane, n - 1);
+      const uint64_t o = off[qc];
+      d.olo = (uint32_t)o;
+      d.ohi = (uint32_t)(o >> 32);
+      d.l = len[qc];
+      d.sd = kSeed ? seed[qc] : 0u;
+      d.lp = kParity ? parity[qc] : 0u;
+    } else {
+      d.sd = kSeed ? seed[min(p0 + lane, n - 1)] : 0u;
+    }
+    return d;
+  };
+  // what a step's sum needs: first aligned chunk, head, end (head + len), 16 x
+  // last chunk, rotation (address parity != logical parity), folded seed
+  struct Z {
+    const uint8_t* c0;
+    uint32_t h, e, lb, rot, sd;
+  };
+  // step j of the super-step at p0 (its packets p0 + 16 j .. + 15)
+  auto geo = [&](const B& d, uint32_t p0, uint32_t j) {
+    const int src = (int)(16u * j + gi);
+    const uint32_t q = p0 + 16u * j + gi;
+    uint64_t o;
+    uint32_t l, lp = 0, sd = 0;
     if constexpr (kStrided) {
-      o = (uint64_t)qc * stride;
+      o = (uint64_t)min(q, n - 1) * stride;
       l = slen;
     } else {
-      o = off[qc];
-      l = len[qc];
+      o = ((uint64_t)(uint32_t)__shfl((int)d.ohi, src) << 32) | (uint32_t)__shfl((int)d.olo, src);
+      l = (uint32_t)__shfl((int)d.l, src);
+      if constexpr (kParity) lp = (uint32_t)__shfl((int)d.lp, src);
     }
+    if constexpr (kSeed) sd = (uint32_t)__shfl((int)d.sd, src);
+    Z z;
+    l = q < n ? l : 0u;
+    // an empty span re-reads the arena's first chunk: its own offset is never
+    // dereferenced
+    const uint8_t* a = base + (l ? o : 0ull);
+    const uint32_t alo = (uint32_t)reinterpret_cast<uintptr_t>(a);
+    z.h = alo & 15u;
+    z.c0 = a - z.h;
+    z.e = z.h + l;
+    z.lb = (max(z.e, 1u) - 1u) & ~15u;
+    z.rot = (lp ^ alo) & 1u;  // in_cksum.c:222-225
+    z.sd = kSeed ? fold16_32(sd) : 0u;
+    return z;
   };
-  uint64_t o_next;
-  uint32_t l_next;
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t p0 = blockIdx.x * kBlock + (threadIdx.x & ~63u);
-  fetch(p0 + lane, o_next, l_next);
-  for (; p0 < n; p0 += step) {
-    const uint32_t q = p0 + lane;  // this lane's packet
-    const bool live = q < n;
-    const uint32_t qc = live ? q : n - 1;
-    const uint64_t o = o_next;
-    uint32_t l = l_next;
-    if (!live) l = 0;
-    const uint64_t oa = o + boff;
-    const uint32_t head = l ? (uint32_t)oa & 15u : 0u;
-    const uint32_t end = head + l;  // bytes [head, end) from the first chunk
-    const uint32_t lastb = (max(end, 1u) - 1u) & ~15u;  // 16 x the last chunk
-    // an empty span (or a dead lane) re-reads the arena's first chunk
-    const uint8_t* c0 = l ? abase + (oa - head) : abase;
-    u32x4 v[kLU];
+  // The empty asm with a memory clobber keeps the loads where they are: with
+  // no store before their use, the compiler otherwise sinks them below the
+  // previous step's sum (its ballot branches), and the pipeline is gone.
+  auto load = [&](const Z& z, u32x4 (&v)[U]) {
 #pragma unroll
-    for (int j = 0; j < kLU; ++j) v[j] = load_chunk(c0 + min(16u * j, lastb));
-    fetch(p0 + step + lane, o_next, l_next);
-    const uint32_t sd = kSeed && live ? seed[qc] : 0u;
-    const uint32_t lp = kParity && live ? parity[qc] : 0u;
-    // chunk j keeps bytes [head - 16 j, end - 16 j): masked unless the whole
-    // wave has it whole (wave-uniform ballots)
+    for (int u = 0; u < U; ++u) v[u] = load_chunk(z.c0 + min(16u * (4u * u + gl), z.lb));
+    asm volatile("" ::: "memory");
+  };
+  // Step j of the block c at p0: round 0 from registers; spans longer than
+  // one round (ragged batches) re-derive their chunk base from the block, so
+  // that only head, end and rotation stay live from a step's load to its sum.
+  auto sum = [&](const Z& z, const u32x4 (&v)[U], const B& c, uint32_t p0,
+                 uint32_t j) -> uint32_t {
     uint32_t acc = 0;
 #pragma unroll
-    for (int j = 0; j < kLU; ++j) {
-      const int s_j = (int)head - 16 * j, e_j = (int)end - 16 * j;
-      if (__ballot(!(s_j <= 0 && e_j >= 16)) == 0)
-        acc = dot_acc(v[j], acc);
-      else
-        acc = dot_acc_masked(v[j], lut.m[MaskLut::index(s_j, e_j)], acc);
+    for (int u = 0; u < U; ++u) {
+      const int cb = (int)(16u * (4u * u + gl));
+      const int s = (int)z.h - cb, e = (int)z.e - cb;
+      if (__ballot(!(s <= 0 && e >= 16)) == 0)  // wave-uniform: every chunk whole
+        acc = dot_acc(v[u], acc);
+      else if (__ballot(e > 0) != 0)  // some lane holds bytes of this slot
+        acc = dot_acc_masked(v[u], lut.m[MaskLut::index(s, e)], acc);
     }
-    if (__ballot(end > 16u * kLU)) {  // spans longer than kLU chunks
-      for (uint32_t k0 = kLU; 16u * k0 < end || __ballot(16u * k0 < end); k0 += kLU) {
-        u32x4 w[kLU];
-#pragma unroll
-        for (int j = 0; j < kLU; ++j) w[j] = load_chunk(c0 + min(16u * (k0 + j), lastb));
-        uint32_t r = 0;
-#pragma unroll
-        for (int j = 0; j < kLU; ++j) {
-          const int b = 16 * (int)(k0 + j);
-          r = dot_acc_masked(w[j], lut.m[MaskLut::index((int)head - b, (int)end - b)], r);
-        }
-        acc = fold16_32(acc) + r;
+    if (__ballot(z.e > kRoundB)) {  // wave-uniform, rare
+      // one chunk per lane per 64-B round, not unrolled: this path's
+      // registers set the kernel's count (U chunks at a time cost 23 VGPRs)
+      const Z y = geo(c, p0, j);
+#pragma unroll 1
+      for (uint32_t rb = kRoundB; __ballot(rb < y.e); rb += 64u) {
+        const uint32_t cb = rb + 16u * gl;
+        const u32x4 w = load_chunk(y.c0 + min(cb, y.lb));
+        acc = fold16_32(acc) +
+              dot_acc_masked(w, lut.m[MaskLut::index((int)(y.h - cb), (int)(y.e - cb))], 0u);
       }
     }
-    uint32_t x = fold16_32(acc);
-    x = fold16_32(x << (8u * ((lp ^ (uint32_t)oa) & 1u)));  // x * 256^rot mod 65535
-    if (kSeed) x = fold16_32(x + fold16_32(sd));
-    uint32_t res = x;
+    return acc;
+  };
+  // Step j's results: reduce, fold, rotate, seed, complement in every lane,
+  // then lane 16 j + i takes packet i's result (quad i) into `res`; `flush`
+  // stores a super-step's 64 results with one coalesced 128-B store.
+  uint32_t res = 0;
+  auto finish = [&](uint32_t x, const Z& z, uint32_t j) {
+    // quad_perm [1,0,3,2] then [2,3,0,1]: every lane holds its packet's total
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xb1, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4e, 0xf, 0xf, false);
+    x = fold16_32(x);
+    x = fold16_32(x << (8u * z.rot));  // x * 256^rot mod 65535
+    if constexpr (kSeed) x = fold16_32(x + z.sd);
+    uint32_t r = x;
     if (!(flags & UINET_CKSUM_F_NO_COMPLEMENT)) {
-      res = ~x & 0xffffu;
-      if ((flags & UINET_CKSUM_F_UDP) && res == 0) res = 0xffff;  // ip_output.c:962-963
+      r = ~x & 0xffffu;
+      if ((flags & UINET_CKSUM_F_UDP) && r == 0) r = 0xffff;  // ip_output.c:962-963
     }
-    if (live) out[q] = (uint16_t)res;
+    r = (uint32_t)__shfl((int)r, (int)(4u * (lane & 15u)));
+    res = (lane >> 4) == j ? r : res;
+  };
+  // lanes past the batch address past the end of the buffer resource: the
+  // hardware drops their writes
+  auto flush = [&](uint32_t p0) {
+    const uint32_t q = p0 + lane;
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, out_rsrc,
+                                          (int)(q < n ? 2u * q : 0xfffffff0u), 0, 0);
+  };
+
+  // the mask table: its words first (L2 hits), then the first step
+  const u32x4* lsrc = reinterpret_cast<const u32x4*>(g_mask_words.w);
+  const u32x4 lw0 = lsrc[threadIdx.x];
+  const u32x4 lw1 = lsrc[min(threadIdx.x + kBlock, 17u * 17u - 1u)];
+  // super-steps of 64 packets; wave w takes super-steps w, w + NW, ... (the
+  // host keeps n + 2 S below 2^32)
+  const uint32_t NW = gridDim.x * kWavesPB;
+  const uint32_t S = 64u * NW;
+  const uint32_t w0 = logical_block(remap) * kWavesPB + rfl(threadIdx.x) / 64;
+  uint32_t p = 64u * w0;
+  u32x4 vA[U], vB[U];
+  Z zA, zB;
+  // two descriptor blocks, ping-pong: a block is reloaded only after its last
+  // use, so no loaded value is ever copied (a copy of the block loaded last
+  // made the compiler wait for every load in flight once per super-step)
+  B b0 = blk(min(p, n - 1));
+  B b1 = blk(min(p + S, n - 1));
+  zA = geo(b0, p, 0);
+  load(zA, vA);
+  lut.m[threadIdx.x] = lw0;
+  // unconditional (threads past the table rewrite its last entry with the
+  // same word): under a branch the compiler sinks lw1's load into it and waits
+  // for every load in flight, the first step's chunks included
+  lut.m[min(threadIdx.x + kBlock, 17u * 17u - 1u)] = lw1;
+  __syncthreads();  // every thread reaches this barrier: no exit before it
+  if (p >= n) return;  // wave-uniform
+  // The four steps of a full super-step at p (step 0 in flight in A), the
+  // next super-step's step 0 (block nx) issued under the last sum.
+  auto super = [&](const B& c, const B& nx) {
+    zB = geo(c, p, 1);
+    load(zB, vB);  // step 1 in flight while step 0 is summed
+    finish(sum(zA, vA, c, p, 0), zA, 0);
+    zA = geo(c, p, 2);
+    load(zA, vA);
+    finish(sum(zB, vB, c, p, 1), zB, 1);
+    zB = geo(c, p, 3);
+    load(zB, vB);
+    finish(sum(zA, vA, c, p, 2), zA, 2);
+    zA = geo(nx, p + S, 0);
+    load(zA, vA);
+    finish(sum(zB, vB, c, p, 3), zB, 3);
+    flush(p);
+    p += S;
+  };
+  // The last super-step: J live steps (1..4), step 0 in flight in A.
+  auto last = [&](const B& c) {
+    const uint32_t J = min((n - p + 15u) / 16u, 4u);
+    if (J == 1) {
+      finish(sum(zA, vA, c, p, 0), zA, 0);
+    } else {
+      zB = geo(c, p, 1);
+      load(zB, vB);
+      finish(sum(zA, vA, c, p, 0), zA, 0);
+      if (J == 2) {
+        finish(sum(zB, vB, c, p, 1), zB, 1);
+      } else {
+        zA = geo(c, p, 2);
+        load(zA, vA);
+        finish(sum(zB, vB, c, p, 1), zB, 1);
+        if (J == 3) {
+          finish(sum(zA, vA, c, p, 2), zA, 2);
+        } else {
+          zB = geo(c, p, 3);
+          load(zB, vB);
+          finish(sum(zA, vA, c, p, 2), zA, 2);
+          finish(sum(zB, vB, c, p, 3), zB, 3);
+        }
+      }
+    }
+    flush(p);
+  };
+  // live super-steps of this wave (>= 1); all but the last have 4 live steps
+  const uint32_t K4 = (n - p + S - 1) / S;
+  uint32_t i = 0;
+  for (; i + 2 < K4; i += 2) {  // super-steps i, i + 1 full, i + 2 live
+    super(b0, b1);
+    b0 = blk(min(p + S, n - 1));  // super-step i + 2
+    super(b1, b0);
+    b1 = blk(min(p + S, n - 1));  // super-step i + 3
+  }
+  if (i + 1 < K4) {  // two live super-steps left
+    super(b0, b1);
+    last(b1);
+  } else {
+    last(b0);
   }
 }
 
 }  // namespace
 
-int launch_spans_lane(const void* base, const uint64_t* off, const uint32_t* len,
+int launch_spans_quad(const void* base, const uint64_t* off, const uint32_t* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
-                      uint32_t flags, bool strided, uint64_t stride, uint32_t slen, int blocks_cu,
-                      hipStream_t stream) {
-  uint64_t blocks = ((uint64_t)n + kBlock - 1) / kBlock;
-  blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, 256ull * (uint64_t)blocks_cu));
+                      uint32_t flags, int u, bool strided, uint64_t stride, uint32_t slen,
+                      int blocks_cu, hipStream_t stream) {
+  constexpr uint32_t kPerBlock = 64u * (kBlock / 64);  // packets per block super-step
+  uint64_t blocks = ((uint64_t)n + kPerBlock - 1) / kPerBlock;
+  // the kernel's 32-bit packet indices need n + 2 * blocks * kPerBlock < 2^32
+  const uint64_t cap = std::min<uint64_t>(256ull * (uint64_t)blocks_cu, (1ull << 26) / kPerBlock);
+  blocks = std::max<uint64_t>(1, std::min(blocks, cap));
   const dim3 grid((uint32_t)blocks), blk(kBlock);
   const uint8_t* b = static_cast<const uint8_t*>(base);
-#define UINET_LANE(P, SD, ST)                                                                  \
-  hipLaunchKernelGGL((k_spans_lane<P, SD, ST>), grid, blk, 0, stream, b, off, len, seed, parity, \
-                     out, n, flags, stride, slen)
-  if (strided) {
-    if (seed) UINET_LANE(false, true, true);
-    else UINET_LANE(false, false, true);
-  } else if (parity) {
-    if (seed) UINET_LANE(true, true, false);
-    else UINET_LANE(true, false, false);
-  } else {
-    if (seed) UINET_LANE(false, true, false);
-    else UINET_LANE(false, false, false);
+  const uint32_t remap = (uint32_t)tuning().xcd_remap;
+#define UINET_QUAD(U, P, SD, ST)                                                             \
+  hipLaunchKernelGGL((k_spans_quad<U, P, SD, ST>), grid, blk, 0, stream, b, off, len, seed, \
+                     parity, out, n, flags, remap, stride, slen)
+#define UINET_QUAD_U(U)                                          \
+  if (strided) {                                                 \
+    if (seed) UINET_QUAD(U, false, true, true);                  \
+    else UINET_QUAD(U, false, false, true);                      \
+  } else if (parity) {                                           \
+    if (seed) UINET_QUAD(U, true, true, false);                  \
+    else UINET_QUAD(U, true, false, false);                      \
+  } else {                                                       \
+    if (seed) UINET_QUAD(U, false, true, false);                 \
+    else UINET_QUAD(U, false, false, false);                     \
   }
-#undef UINET_LANE
+  if (u == 1) {
+    UINET_QUAD_U(1)
+  } else {
+    UINET_QUAD_U(2)
+  }
+#undef UINET_QUAD_U
+#undef UINET_QUAD
   return check_launch();
 }
 

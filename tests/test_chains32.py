@@ -83,13 +83,13 @@ def test_chains32_len_skip_seed(torch_dev, ora, hint):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,long_ch,tile", [(0, 128, 0), (0, 16, 8), (0, 0, 32), (1, 128, 0), (2, 128, 0), (3, 128, 0), (3, 16, 8), (3, 0, 32),
-                                                   (2, 16, 8), (2, 0, 32)])
-def test_chains32_long_and_many_segments(torch_dev, ora, variant, long_ch, tile):
+@pytest.mark.parametrize("cpass,long_ch,tile", [(2, 128, 0), (2, 16, 8), (2, 0, 32), (4, 128, 0),
+                                                 (4, 16, 8), (4, 0, 32)])
+def test_chains32_long_and_many_segments(torch_dev, ora, cpass, long_ch, tile):
     """Segments up to 65535 B (the u16 limit) mixed with 0..3-B ones, chains of
-    up to 200 segments across descriptor rounds, every kernel variant."""
+    up to 200 segments across descriptor rounds, both batch widths."""
     torch = torch_dev
-    rng = np.random.default_rng(9200 + 7 * variant + long_ch + tile)
+    rng = np.random.default_rng(9200 + 7 * cpass + long_ch + tile)
     arena = rand_arena(1 << 23, 62)
     n = 900
     nseg = rng.integers(0, 200, n)
@@ -110,7 +110,7 @@ def test_chains32_long_and_many_segments(torch_dev, ora, variant, long_ch, tile)
     d_len, d_skip = dev(torch, length.astype(np.int32)), dev(torch, skip.astype(np.int32))
     d_seed = dev(torch, seed.view(np.int32))
     so, sl = packed_dev(torch, seg_off, seg_len)
-    u.set_tuning("chains_variant", variant)
+    u.set_tuning("chains_pass", cpass)
     u.set_tuning("chains_long", long_ch)
     u.set_tuning("chains_tile", tile)
     try:
@@ -121,7 +121,7 @@ def test_chains32_long_and_many_segments(torch_dev, ora, variant, long_ch, tile)
                                  flags=flags, len_hint=200)
             np.testing.assert_array_equal(host16(got), want)
     finally:
-        u.set_tuning("chains_variant", 0)
+        u.set_tuning("chains_pass", 2)
         u.set_tuning("chains_long", 128)
         u.set_tuning("chains_tile", 0)
 

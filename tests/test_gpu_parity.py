@@ -84,38 +84,42 @@ def test_spans_no_seed_no_parity(torch_dev, ora, hint):
     np.testing.assert_array_equal(host16(got), want)
 
 
+@pytest.mark.parametrize("pipe", [0, 1, 2])
 @pytest.mark.parametrize("n", [1, 7, 6000, 70001])
-def test_spans_contig_order(torch_dev, ora, n):
-    """Block-contiguous packet order (spans_contig=1) at every geometry and
-    for the strided kernel: every packet folded exactly once, ragged tails."""
+def test_spans_every_kernel(torch_dev, ora, n, pipe):
+    """Every span kernel family (spans_pipe 1 lean / quad, 2 k_spans_pp, 0
+    one-shot) at every geometry, and the strided kernel at 64 and 60 B: each
+    packet folded exactly once, ragged tails."""
     torch = torch_dev
-    rng = np.random.default_rng(500 + n)
+    rng = np.random.default_rng(500 + n + 7 * pipe)
     arena = rand_arena(1 << 21, 31)
     off, ln = rand_spans(rng, n, arena.size, 1600)
     want = ora.spans(arena, off, ln)
     d_arena = dev(torch, arena)
-    u.set_tuning("spans_contig", 1)
+    u.set_tuning("spans_pipe", pipe)
     try:
         for hint in HINTS:
             got = u.cksum_spans(d_arena, dev(torch, off), dev(torch, ln.astype(np.int32)),
                                 len_hint=hint)
             np.testing.assert_array_equal(host16(got), want)
         m = min(n, (arena.size - 64) // 64)
-        got = u.cksum_strided(d_arena, 64, 60, m)
-        want_s = ora.spans(arena, 64 * np.arange(m, dtype=np.int64), np.full(m, 60, np.int64))
-        np.testing.assert_array_equal(host16(got), want_s)
+        for length in (64, 60):
+            got = u.cksum_strided(d_arena, 64, length, m)
+            want_s = ora.spans(arena, 64 * np.arange(m, dtype=np.int64),
+                               np.full(m, length, np.int64))
+            np.testing.assert_array_equal(host16(got), want_s)
     finally:
-        u.set_tuning("spans_contig", 0)
+        u.set_tuning("spans_pipe", 1)
 
 
-@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0), (2, 1), (2, 0),
-                                      (3, 1), (3, 3), (3, 0)])
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0), (2, 1), (2, 3),
+                                      (2, 0)])
 def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
-    """The persistent two-in-flight span kernel (spans_pipe=1, the default
-    for 32 and 64 lanes per packet), the wave-per-packet kernel (2) and the
-    one-packet-per-group kernel (0), on
-    grids small enough that every lane group walks many packets: ragged
-    batches, seeds, parity, UDP, spans longer than one round, empty spans."""
+    """The persistent span kernels at 32 and 64 lanes per packet (spans_pipe
+    1 k_spans_lean, the default; 2 k_spans_pp) and the one-packet-per-group
+    kernel (0), on grids small enough that every wave walks many steps:
+    ragged batches, seeds, parity, UDP, spans longer than one round, empty
+    spans."""
     torch = torch_dev
     rng = np.random.default_rng(700 + 10 * pipe + bpc)
     arena = rand_arena(1 << 22, 41)
@@ -139,11 +143,11 @@ def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
         u.set_tuning("blocks_per_cu", 0)
 
 
-@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0), (3, 1), (3, 3),
-                                      (3, 0)])
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0), (2, 1), (2, 3),
+                                      (2, 0)])
 def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
-    """The strided API on the persistent two-in-flight kernel (spans_pipe=1,
-    32 / 64 lanes per packet) and on the one-shot kernel (0), with grids small
+    """The strided API on the persistent kernels (spans_pipe 1 k_spans_lean,
+    2 k_spans_pp; 32 / 64 lanes per packet) and on the one-shot kernel (0), with grids small
     enough that every lane group walks many packets: packet lengths of one
     round and of several, aligned and unaligned strides and bases, seeds and
     UDP, ragged counts."""
@@ -169,11 +173,12 @@ def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
         u.set_tuning("blocks_per_cu", 0)
 
 
-@pytest.mark.parametrize("pipe", [1, 3])
+@pytest.mark.parametrize("pipe", [1, 2])
 def test_spans_far_apart(torch_dev, ora, pipe):
-    """Neighbouring packets (one wave's pair at 32 lanes per packet) that lie
-    4 GiB and more apart in one arena: the lean kernel's loads are relative
-    to one scalar base, and such a pair takes its 64-bit fallback."""
+    """Neighbouring packets (one wave's pair at 32 lanes per packet, one
+    wave's 16 at 4) that lie 4 GiB and more apart in one arena: the lean
+    kernel's loads are relative to one scalar base, and such a pair takes its
+    64-bit fallback."""
     torch = torch_dev
     rng = np.random.default_rng(4242)
     win = 1 << 16
@@ -194,7 +199,7 @@ def test_spans_far_apart(torch_dev, ora, pipe):
     par = rng.integers(0, 2, n).astype(np.uint8)
     u.set_tuning("spans_pipe", pipe)
     try:
-        for hint in (1500, 9000):
+        for hint in (64, 1500, 9000):
             got = u.cksum_spans(d, dev(torch, off_dev), dev(torch, ln.astype(np.int32)),
                                 seed=dev(torch, seed.view(np.int32)), parity=dev(torch, par),
                                 flags=u.F_UDP, len_hint=hint)
@@ -206,18 +211,21 @@ def test_spans_far_apart(torch_dev, ora, pipe):
         torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("pipe", [1, 3])
-def test_spans_small_packets(torch_dev, ora, pipe):
-    """The small-packet geometries (4, 8 and 16 lanes per packet; with
-    spans_pipe=3 the 4-lane shapes run the lane-per-packet kernel): ragged
-    counts, spans longer than the geometry's round, empty spans, seeds,
-    parity, UDP; the strided API at 64-B packets, 16-B aligned and not."""
+@pytest.mark.parametrize("pipe,bpc", [(1, 0), (1, 1), (1, 3), (0, 0), (2, 0)])
+def test_spans_small_packets(torch_dev, ora, pipe, bpc):
+    """The small-packet geometries (4, 8 and 16 lanes per packet; the 4-lane
+    shapes run k_spans_quad under spans_pipe=1, k_spans otherwise), also on
+    grids small enough that every wave walks many steps: ragged counts, spans
+    longer than the geometry's round, empty spans, seeds, parity, UDP; the
+    strided API at 64-B packets, 16-B aligned and not."""
     torch = torch_dev
     u.set_tuning("spans_pipe", pipe)
+    u.set_tuning("blocks_per_cu", bpc)
     try:
         _small_packets(torch, ora)
     finally:
         u.set_tuning("spans_pipe", 1)
+        u.set_tuning("blocks_per_cu", 0)
 
 
 def _small_packets(torch, ora):
@@ -698,12 +706,12 @@ def test_zero_copy_pipeline_ring(torch_dev, ora, host_threads):
         np.testing.assert_array_equal(got[("hdr", k)], want_hdr)
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3])
+@pytest.mark.parametrize("cpass", [2, 4])
 @pytest.mark.parametrize("long_ch,tile", [(0, 32), (16, 8), (16, 32), (64, 0), (200, 8)])
-def test_chains_long_segments(torch_dev, ora, long_ch, tile, variant):
+def test_chains_long_segments(torch_dev, ora, long_ch, tile, cpass):
     """Chains mixing short and long (wave-streamed) segments, with len/skip
     clipping that cuts into long segments, over both tile sizes and both
-    segment lookups of the chunk-stream kernel."""
+    batch widths (chains_pass) of the chunk-stream kernel."""
     torch = torch_dev
     rng = np.random.default_rng(5100 + long_ch + tile)
     arena = rand_arena(1 << 23, 51)
@@ -720,7 +728,7 @@ def test_chains_long_segments(torch_dev, ora, long_ch, tile, variant):
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
     u.set_tuning("chains_long", long_ch)
     u.set_tuning("chains_tile", tile)
-    u.set_tuning("chains_variant", variant)
+    u.set_tuning("chains_pass", cpass)
     try:
         for flags in (0, u.F_UDP):
             w = want if flags == 0 else ora.chains(arena, seg_off, seg_len, pkt_seg, length=length,
@@ -735,18 +743,17 @@ def test_chains_long_segments(torch_dev, ora, long_ch, tile, variant):
     finally:
         u.set_tuning("chains_long", 128)
         u.set_tuning("chains_tile", 0)
-        u.set_tuning("chains_variant", 0)
+        u.set_tuning("chains_pass", 2)
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3])
+@pytest.mark.parametrize("cpass", [2, 4])
 @pytest.mark.parametrize("long_ch", [0, 200])
-def test_chains_full_rounds(torch_dev, ora, long_ch, variant):
+def test_chains_full_rounds(torch_dev, ora, long_ch, cpass):
     """Descriptor rounds whose chunk list is longer than 4096 chunks: 64
-    segments of 1900-2031 B each (up to 127 chunks, the most a list segment
-    of the bitmap lookup holds), so the lookup crosses its 64-word bitmap
-    window; mixed with rounds of tiny and empty segments."""
+    segments of 1900-2031 B each (up to 127 chunks), mixed with rounds of tiny
+    and empty segments."""
     torch = torch_dev
-    rng = np.random.default_rng(6100 + long_ch + variant)
+    rng = np.random.default_rng(6100 + long_ch + cpass)
     arena = rand_arena(1 << 24, 61)
     n = 2048
     nseg = rng.integers(1, 9, n)
@@ -760,7 +767,7 @@ def test_chains_full_rounds(torch_dev, ora, long_ch, variant):
     length = np.where(rng.random(n) < 0.7, tot, skip + (rng.random(n) * (tot - skip + 1)).astype(np.int64))
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip)
     u.set_tuning("chains_long", long_ch)
-    u.set_tuning("chains_variant", variant)
+    u.set_tuning("chains_pass", cpass)
     u.set_tuning("chains_tile", 32)  # 32 packets x ~5 segments: full 64-segment rounds
     try:
         got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off),
@@ -771,17 +778,16 @@ def test_chains_full_rounds(torch_dev, ora, long_ch, variant):
         np.testing.assert_array_equal(host16(got), want)
     finally:
         u.set_tuning("chains_long", 128)
-        u.set_tuning("chains_variant", 0)
+        u.set_tuning("chains_pass", 2)
         u.set_tuning("chains_tile", 0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
-def test_chains_kernel_variants(torch_dev, ora, variant):
-    """The chain kernels (0 chunk stream, 1 serial walk, 2 chunk stream with
-    the bitmap segment lookup) on chains of 0..150 segments with
-    len/skip/seed and the UDP flag."""
+@pytest.mark.parametrize("cpass", [2, 4])
+def test_chains_kernel_variants(torch_dev, ora, cpass):
+    """The chain kernel at both batch widths (chains_pass) on chains of
+    0..150 segments with len/skip/seed and the UDP flag."""
     torch = torch_dev
-    rng = np.random.default_rng(8800 + variant)
+    rng = np.random.default_rng(8800 + cpass)
     arena = rand_arena(1 << 21, 47)
     n = 1500
     nseg = rng.integers(0, 151, n)
@@ -796,7 +802,7 @@ def test_chains_kernel_variants(torch_dev, ora, variant):
     skip = (rng.random(n) * (tot + 1) * 0.3).astype(np.int64)
     length = skip + (rng.random(n) * (tot - skip + 10)).astype(np.int64)
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
-    u.set_tuning("chains_variant", variant)
+    u.set_tuning("chains_pass", cpass)
     try:
         for flags in (0, u.F_UDP):
             want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip,
@@ -809,7 +815,7 @@ def test_chains_kernel_variants(torch_dev, ora, variant):
                                  seed=dev(torch, seed.view(np.int32)), flags=flags, len_hint=120)
             np.testing.assert_array_equal(host16(got), want)
     finally:
-        u.set_tuning("chains_variant", 0)
+        u.set_tuning("chains_pass", 2)
 
 
 def test_chains_beyond_4gib_window(torch_dev, ora):
@@ -838,21 +844,22 @@ def test_chains_beyond_4gib_window(torch_dev, ora):
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     skip = np.full(n, 3, np.int64)
     want = ora.chains(host, seg_off, seg_len, pkt_seg, skip=skip, seed=seed)
-    for variant in (0, 1, 2, 3):
-        u.set_tuning("chains_variant", variant)
+    for cpass in (2, 4):
+        u.set_tuning("chains_pass", cpass)
         try:
             got = u.cksum_chains(d, dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
                                  dev(torch, pkt_seg.astype(np.int32)),
                                  skip=dev(torch, skip.astype(np.int32)),
                                  seed=dev(torch, seed.view(np.int32)), len_hint=150)
         finally:
-            u.set_tuning("chains_variant", 0)
+            u.set_tuning("chains_pass", 2)
         np.testing.assert_array_equal(host16(got), want)
     # spans and strided packets past the 4 GiB mark (64-bit offsets)
     off = rng.integers((1 << 32) - 4096, size - 10000, 3000).astype(np.int64)
     ln = rng.integers(0, 9000, 3000)
-    got = u.cksum_spans(d, dev(torch, off), dev(torch, ln.astype(np.int32)), len_hint=4000)
-    np.testing.assert_array_equal(host16(got), ora.spans(host, off, ln))
+    for hint in (64, 4000):
+        got = u.cksum_spans(d, dev(torch, off), dev(torch, ln.astype(np.int32)), len_hint=hint)
+        np.testing.assert_array_equal(host16(got), ora.spans(host, off, ln))
     got = u.cksum_strided(d[(1 << 32) - 7:], 1514, 1500, 2000)
     np.testing.assert_array_equal(
         host16(got), ora.spans(host, (1 << 32) - 7 + 1514 * np.arange(2000), 1500))
