@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=200,
                     help="untimed steps first: the first ~30-100 back-to-back launches run "
                     "up to 25 %% slower while clocks settle (tools/drift.py)")
-    ap.add_argument("--config", choices=["2", "2rx", "2s", "3", "3tx", "4", "5", "5tso"],
+    ap.add_argument("--config", choices=["2", "2rx", "2s", "2su", "3", "3tx", "4", "5", "5tso"],
                     default=None,
                     help="BASELINE.json config shape (default: 2 = the headline at N = 1, 4 = "
                     "2,097,152 packets per GPU when distributed; 2s = 16 M x 64 B packets, a "
@@ -120,11 +120,15 @@ def build_workload(cfg: str, n, rank: int, world: int = 1):
         w["desc"] = (f"config{cfg}: {n:,} x 1500 B contiguous packets (stride {w['stride']}"
                      f"{', +14' if cfg == '2rx' else ''}), device-resident, in_cksum_skip(m,1500,0)")
         w["hint"] = 1500
-    elif cfg == "2s":
+    elif cfg in ("2s", "2su"):
         n = n or (1 << 24)
-        w = W.config2_device(n, stride=64, length=64, rank=rank)
-        w["desc"] = (f"config2s: {n:,} x 64 B contiguous packets (stride 64), device-resident, "
-                     f"in_cksum_skip(m,64,0) -- small-packet shape, not a BASELINE.json config")
+        # 2su: the same packets 2 B off 16-B alignment (an IP packet behind a
+        # 14-B Ethernet header at a 16-B aligned frame): every span touches 5 chunks
+        base = 2 if cfg == "2su" else 0
+        w = W.config2_device(n, stride=64, length=64, base=base, rank=rank)
+        w["desc"] = (f"config{cfg}: {n:,} x 64 B contiguous packets (stride 64"
+                     f"{', +2' if base else ''}), device-resident, in_cksum_skip(m,64,0) -- "
+                     f"small-packet shape, not a BASELINE.json config")
         w["hint"] = 64
     elif cfg == "3":
         n = n or (1 << 20)
@@ -161,7 +165,7 @@ def make_launch(cfg: str, w, api: str, out, desc: str = "wide"):
         return lambda s: u.cksum_chains(w["arena"], so, sl, w["pkt_seg"],
                                         length=w["len"], skip=w["skip"], seed=w.get("seed"),
                                         out=out, len_hint=w["hint"], stream=s)
-    if api == "strided" and cfg in ("2", "2rx", "2s"):
+    if api == "strided" and cfg in ("2", "2rx", "2s", "2su"):
         base = w["arena"][w["base"]:]
         return lambda s: u.cksum_strided(base, w["stride"], w["length"], w["n"], out=out, stream=s)
     seed = w.get("seed")
@@ -354,7 +358,7 @@ def main():
             dist.init_process_group("gloo")
         plan = {"rank": rank, "local_rank": local,
                 "world": dist.get_world_size() if distributed else 1, "config": args.config,
-                "packets_per_gpu": args.packets or {"4": 1 << 21, "2s": 1 << 24,
+                "packets_per_gpu": args.packets or {"4": 1 << 21, "2s": 1 << 24, "2su": 1 << 24,
                                                     "5": 131072}.get(args.config, 1 << 20),
                 "backend": os.environ.get("UINET_BENCH_BACKEND", "nccl") if distributed else None}
         print(json.dumps(plan), flush=True)

@@ -173,13 +173,14 @@ struct SpanPP {
   int head, end;  // the span's bytes are [head, end) from its first aligned chunk
   u32x4 v[U];
   // Loads the span's first G * U chunks (an empty span re-reads the arena's
-  // first chunk; lanes past the end re-read the last chunk) and keeps only
-  // what the fold needs.
+  // first aligned chunk -- base itself may be unaligned, and an unaligned
+  // 16-B read may cross into an unmapped page; lanes past the end re-read
+  // the last chunk) and keeps only what the fold needs.
   __device__ __forceinline__ void load(const uint8_t* base, uint64_t o, uint32_t len, int gl) {
     const uint8_t* a = base + o;
     head = len ? (int)(reinterpret_cast<uintptr_t>(a) & 15) : 0;
     end = head + (int)len;
-    const uint8_t* c0 = len ? a - head : base;
+    const uint8_t* c0 = len ? a - head : base - (reinterpret_cast<uintptr_t>(base) & 15);
     const uint32_t last = len ? ((uint32_t)(end + 15) >> 4) - 1u : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = load_chunk(c0 + 16u * min((uint32_t)(u * G + gl), last));
@@ -363,11 +364,11 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   // 0.2095; on a slower stretch of the same box +1.4 %.
   if (pipe == 1 && geo.g == 4)
     return launch_spans_quad(base, off, len, seed, parity, out, n, flags, geo.u, false, 0, 0,
-                             blocks_per_cu(32), stream);
+                             blocks_per_cu(128), stream);
   const bool sdesc = tuning().spans_sdesc && geo.g >= 32;
   if (sdesc && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, false, 0, 0,
-                             blocks_per_cu(128), stream);
+                             blocks_per_cu(512), stream);
   if (sdesc && pipe) {
     const int grid = grid_for(n, geo.g, 128);
 #define LP(G, U)                                                                          \
@@ -410,12 +411,14 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   if (len <= 64 && ((reinterpret_cast<uintptr_t>(base) | pkt_stride) & 15) == 0) geo = {4, 1};
   geo = geometry_override(geo);
   const int pipe = tuning().spans_pipe;
-  if (pipe == 1 && geo.g == 4)
-    return launch_spans_quad(base, nullptr, nullptr, seed, nullptr, out, n, flags, geo.u, true,
-                             pkt_stride, len, blocks_per_cu(32), stream);
+  // k_spans_quad for 16-B aligned packets of <= 64 B (one chunk per lane);
+  // unaligned ones run k_spans<4, 2>, 5 % faster there (profiles/r03/r03p/)
+  if (pipe == 1 && geo.g == 4 && geo.u == 1)
+    return launch_spans_quad(base, nullptr, nullptr, seed, nullptr, out, n, flags, 1, true,
+                             pkt_stride, len, blocks_per_cu(128), stream);
   if (geo.g >= 32 && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, nullptr, nullptr, seed, nullptr, out, n, flags, geo.g, true,
-                             pkt_stride, len, blocks_per_cu(128), stream);
+                             pkt_stride, len, blocks_per_cu(512), stream);
   if (geo.g >= 32 && pipe) {
     // the persistent two-in-flight groups of k_spans_pp, descriptors from
     // the stride: as for the span API, the one-shot grid (spans_pipe = 0)

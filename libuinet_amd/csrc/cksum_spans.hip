@@ -408,20 +408,24 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   // wait for the loads in flight) and no step past the end is ever loaded:
   // the last one or two steps run after the loop.  Descriptors are fetched
   // two steps ahead (clamped to the batch: a clamped fetch is never loaded).
-  //
+  const uint32_t qmax = (n - 1) & ~(uint32_t)(kP - 1);  // the last step start
+  u32x4 vA[kU], vB[kU];
+  Geo<kP> zA;
   // The block's mask table: its words are loaded first (L2 hits), then the
   // first step's chunks, and the table is written to LDS while those are in
   // flight (the wait before the writes covers only the table's loads).
+  // Computing it instead (30 VALU per entry) measured 2 % faster warm at 512
+  // blocks per CU but slower in the driver's window (0.864 / 0.869 against
+  // 0.889 / 0.872, profiles/r03/r03m/); 1024-thread blocks were no better at
+  // 128 per CU and 13 % slower at 512 (r03l/).
   const u32x4* lsrc = reinterpret_cast<const u32x4*>(g_mask_words.w);
   const u32x4 lw0 = lsrc[threadIdx.x];
   const u32x4 lw1 = lsrc[min(threadIdx.x + kBlock, 17u * 17u - 1u)];
-  const uint32_t qmax = (n - 1) & ~(uint32_t)(kP - 1);  // the last step start
-  u32x4 vA[kU], vB[kU];
-  Geo<kP> zA = load_step(desc(min(q, qmax)), vA);
+  zA = load_step(desc(min(q, qmax)), vA);
   lut.m[threadIdx.x] = lw0;
   // unconditional (threads past the table rewrite its last entry with the
-  // same word): under a branch the compiler sinks lw1's load into it and waits
-  // for every load in flight, the first step's chunks included
+  // same word): under a branch the compiler sinks lw1's load into it and
+  // waits for every load in flight, the first step's chunks included
   lut.m[min(threadIdx.x + kBlock, 17u * 17u - 1u)] = lw1;
   __syncthreads();  // every thread reaches this barrier: no exit before it
   if (q >= n) return;  // wave-uniform
@@ -458,13 +462,16 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
 //    vector load per array, one lane per packet, issued a whole super-step
 //    before its first step; a step's quads take their packet's words with
 //    ds_bpermute.  (Per-step descriptor loads, issued one step ahead, chained
-//    each step's chunk loads to a descriptor round trip: ~1 KiB per wave per
-//    memory latency, 20 % slower than k_spans on config 2s.)
-//  * a lane's U chunk slots are chunks gl, 4 + gl (64-bit addresses, clamped
-//    to the packet's last chunk); a slot that every lane holds whole skips the
-//    mask table, one that every lane holds empty skips the sum (ballots);
-//  * step k + 1's chunks are loaded before step k is summed; no load sits
-//    under a branch in the loop;
+//    each step's chunk loads to a descriptor round trip.)
+//  * a lane's chunk slots are chunks gl and 4 + gl (64-bit addresses,
+//    clamped to the packet's last chunk).  Slot 1 is loaded only when some
+//    span of the step reaches past 64 B: unconditional, its redundant loads
+//    made aligned 64-B packets 13-23 % slower (profiles/r03/r03o/, r03p/).  A
+//    slot that every lane holds whole skips the mask table, one that every
+//    lane holds empty skips the sum (ballots);
+//  * step k + 1's chunks are loaded before step k is summed;
+//  * a step with a span longer than one round (ragged batches) is marked and
+//    redone whole at the end of its super-step, where few registers are live;
 //  * a packet's 4 lane partials meet in 2 DPP quad_perm adds, and the fold,
 //    rotation, seed and complement run branch-free in every lane; lane i
 //    collects packet i's result of the super-step (one ds_bpermute per step)
@@ -542,15 +549,18 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
   // no store before their use, the compiler otherwise sinks them below the
   // previous step's sum (its ballot branches), and the pipeline is gone.
   auto load = [&](const Z& z, u32x4 (&v)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = load_chunk(z.c0 + min(16u * (4u * u + gl), z.lb));
+    v[0] = load_chunk(z.c0 + min(16u * gl, z.lb));
+    // slot 1 only when some span of the step reaches past 64 B (wave-uniform):
+    // aligned 64-B packets never need it
+    if constexpr (U == 2)
+      if (__ballot(z.e > 64u)) v[1] = load_chunk(z.c0 + min(16u * (4u + gl), z.lb));
     asm volatile("" ::: "memory");
   };
-  // Step j of the block c at p0: round 0 from registers; spans longer than
-  // one round (ragged batches) re-derive their chunk base from the block, so
-  // that only head, end and rotation stay live from a step's load to its sum.
-  auto sum = [&](const Z& z, const u32x4 (&v)[U], const B& c, uint32_t p0,
-                 uint32_t j) -> uint32_t {
+  // Round 0 of a step from registers.  A step with a span longer than one
+  // round (ragged batches) is marked pending and redone whole at the end of
+  // its super-step (`redo`): inlined at every step, that path's registers
+  // were the kernel's count (84 VGPRs against 70 without it).
+  auto sum = [&](const Z& z, const u32x4 (&v)[U], uint32_t j, uint32_t& pend) -> uint32_t {
     uint32_t acc = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -561,17 +571,18 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
       else if (__ballot(e > 0) != 0)  // some lane holds bytes of this slot
         acc = dot_acc_masked(v[u], lut.m[MaskLut::index(s, e)], acc);
     }
-    if (__ballot(z.e > kRoundB)) {  // wave-uniform, rare
-      // one chunk per lane per 64-B round, not unrolled: this path's
-      // registers set the kernel's count (U chunks at a time cost 23 VGPRs)
-      const Z y = geo(c, p0, j);
+    if (__ballot(z.e > kRoundB)) pend |= 1u << j;  // wave-uniform
+    return acc;
+  };
+  // A pending step's whole sum, one chunk per lane per 64-B round.
+  auto full_sum = [&](const Z& y) -> uint32_t {
+    uint32_t acc = 0;
 #pragma unroll 1
-      for (uint32_t rb = kRoundB; __ballot(rb < y.e); rb += 64u) {
-        const uint32_t cb = rb + 16u * gl;
-        const u32x4 w = load_chunk(y.c0 + min(cb, y.lb));
-        acc = fold16_32(acc) +
-              dot_acc_masked(w, lut.m[MaskLut::index((int)(y.h - cb), (int)(y.e - cb))], 0u);
-      }
+    for (uint32_t rb = 0; __ballot(rb < y.e); rb += 64u) {
+      const uint32_t cb = rb + 16u * gl;
+      const u32x4 w = load_chunk(y.c0 + min(cb, y.lb));
+      acc = fold16_32(acc) +
+            dot_acc_masked(w, lut.m[MaskLut::index((int)(y.h - cb), (int)(y.e - cb))], 0u);
     }
     return acc;
   };
@@ -593,6 +604,15 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
     }
     r = (uint32_t)__shfl((int)r, (int)(4u * (lane & 15u)));
     res = (lane >> 4) == j ? r : res;
+  };
+  // the pending steps of the super-step at p0 (block c), redone whole
+  auto redo = [&](const B& c, uint32_t p0, uint32_t pend) {
+#pragma unroll 1
+    for (uint32_t j = 0; j < 4; ++j)
+      if (pend & (1u << j)) {
+        const Z y = geo(c, p0, j);
+        finish(full_sum(y), y, j);
+      }
   };
   // lanes past the batch address past the end of the buffer resource: the
   // hardware drops their writes
@@ -631,46 +651,50 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
   // The four steps of a full super-step at p (step 0 in flight in A), the
   // next super-step's step 0 (block nx) issued under the last sum.
   auto super = [&](const B& c, const B& nx) {
+    uint32_t pend = 0;
     zB = geo(c, p, 1);
     load(zB, vB);  // step 1 in flight while step 0 is summed
-    finish(sum(zA, vA, c, p, 0), zA, 0);
+    finish(sum(zA, vA, 0, pend), zA, 0);
     zA = geo(c, p, 2);
     load(zA, vA);
-    finish(sum(zB, vB, c, p, 1), zB, 1);
+    finish(sum(zB, vB, 1, pend), zB, 1);
     zB = geo(c, p, 3);
     load(zB, vB);
-    finish(sum(zA, vA, c, p, 2), zA, 2);
+    finish(sum(zA, vA, 2, pend), zA, 2);
     zA = geo(nx, p + S, 0);
     load(zA, vA);
-    finish(sum(zB, vB, c, p, 3), zB, 3);
+    finish(sum(zB, vB, 3, pend), zB, 3);
+    if (pend) redo(c, p, pend);  // wave-uniform, rare
     flush(p);
     p += S;
   };
   // The last super-step: J live steps (1..4), step 0 in flight in A.
   auto last = [&](const B& c) {
+    uint32_t pend = 0;
     const uint32_t J = min((n - p + 15u) / 16u, 4u);
     if (J == 1) {
-      finish(sum(zA, vA, c, p, 0), zA, 0);
+      finish(sum(zA, vA, 0, pend), zA, 0);
     } else {
       zB = geo(c, p, 1);
       load(zB, vB);
-      finish(sum(zA, vA, c, p, 0), zA, 0);
+      finish(sum(zA, vA, 0, pend), zA, 0);
       if (J == 2) {
-        finish(sum(zB, vB, c, p, 1), zB, 1);
+        finish(sum(zB, vB, 1, pend), zB, 1);
       } else {
         zA = geo(c, p, 2);
         load(zA, vA);
-        finish(sum(zB, vB, c, p, 1), zB, 1);
+        finish(sum(zB, vB, 1, pend), zB, 1);
         if (J == 3) {
-          finish(sum(zA, vA, c, p, 2), zA, 2);
+          finish(sum(zA, vA, 2, pend), zA, 2);
         } else {
           zB = geo(c, p, 3);
           load(zB, vB);
-          finish(sum(zA, vA, c, p, 2), zA, 2);
-          finish(sum(zB, vB, c, p, 3), zB, 3);
+          finish(sum(zA, vA, 2, pend), zA, 2);
+          finish(sum(zB, vB, 3, pend), zB, 3);
         }
       }
     }
+    if (pend) redo(c, p, pend);
     flush(p);
   };
   // live super-steps of this wave (>= 1); all but the last have 4 live steps

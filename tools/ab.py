@@ -18,6 +18,14 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+# the engine's knob defaults (include/uinet_cksum.h); host_threads defaults to
+# min(16, hardware threads)
+DEFAULTS = {"blocks_per_cu": 0, "chains_pass": 2, "chains_long": 128, "chains_tile": 0,
+            "xcd_remap": 1, "spans_geo": 0, "spans_sdesc": 1, "spans_pipe": 1,
+            "walk_prefetch": 1, "host_group": 1, "host_pin": 0, "multi_gather": 0,
+            "host_threads": min(16, os.cpu_count() or 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="2")
@@ -37,10 +45,19 @@ def main():
     launch = bench.make_launch(a.config, w, a.api, out)
     variants = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(",") if kv)
                 for v in a.variants]
+    # Every key any variant names goes back to its default before each variant
+    # is applied.  (Until round 3 a variant inherited the keys the previous one
+    # had set, so e.g. "spans_pipe=1" after "blocks_per_cu=4096" ran at 4096.)
+    for v in variants:
+        for k in v:
+            if k not in DEFAULTS:
+                raise SystemExit(f"tools/ab.py: no default recorded for knob {k!r}")
     times = {i: [] for i in range(len(variants))}
     ref = None
     for r in range(a.rounds):
         for i, v in enumerate(variants):
+            for k in {k for vv in variants for k in vv}:
+                u.set_tuning(k, DEFAULTS[k])
             for k, val in v.items():
                 u.set_tuning(k, val)
             launch(s)  # warm
