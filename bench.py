@@ -179,14 +179,46 @@ def kernel_name(cfg: str, api: str, desc: str = "wide") -> str:
     return "k_strided" if api == "strided" else "k_spans"
 
 
-def load_traffic(path: str, key: str):
+def dispatched_kernel(cfg: str, api: str, w) -> str:
+    """The kernel family the engine launches for this line (mirrors
+    launch_spans / launch_strided / launch_chains in libuinet_amd/csrc and the
+    UINET_CKSUM_SPANS_PIPE / UINET_CKSUM_SPANS_GEO knobs)."""
+    if cfg in CHAIN_CONFIGS:
+        return "k_chains_pipe"
+    pipe = int(os.environ.get("UINET_CKSUM_SPANS_PIPE", "1") or 1)
+    geo = int(os.environ.get("UINET_CKSUM_SPANS_GEO", "0") or 0)
+    mean = w["length"] if api == "strided" else w["hint"]
+    g = 4 if mean <= 64 else 8 if mean <= 224 else 16 if mean <= 720 else 32 if mean <= 1520 else 64
+    u = 2 if g == 4 else 3
+    if api == "strided" and mean <= 64 and (w["base"] | w["stride"]) % 16 == 0:
+        u = 1
+    if geo:
+        g, u = geo // 16, geo % 16
+    if g >= 32:
+        if pipe == 1 and u == 3:
+            return "k_spans_lean"
+        return {0: "k_spans", 1: "k_spans_pp", 2: "k_spans_pp"}[pipe]
+    if g == 4 and pipe == 1 and (api == "spans" or u == 1):
+        return "k_spans_quad"
+    return "k_spans"
+
+
+def load_traffic(path: str, key: str, kernel: str):
+    """HBM bytes per launch from the FETCH_SIZE passes folded into `path`
+    (tools/prof_all.sh), with where they were measured; None when the entry
+    was measured on a different kernel than the one this line launched."""
     try:
         with open(path) as f:
-            d = json.load(f)
-        e = d.get(key)
-        return None if e is None else float(e["hbm_read_bytes_per_launch"])
+            e = json.load(f).get(key)
     except Exception:
-        return None
+        e = None
+    if e is None:
+        return None, {"key": key, "note": "no FETCH_SIZE entry"}
+    src = {"key": key, "source": e.get("source"), "measured_kernel": e.get("kernel")}
+    if not str(e.get("kernel", "")).startswith(kernel + "<"):
+        src["note"] = "measured on another kernel: not reported"
+        return None, src
+    return float(e["hbm_read_bytes_per_launch"]), src
 
 
 def layout_floor_line(cfg: str, w, desc: str, kms) -> dict:
@@ -484,7 +516,8 @@ def main():
         value = total_bytes / elapsed / 2**30
         achieved = w["bytes"] / (kms.mean() * 1e-3) / 1e9
         key = f"{kernel_name(args.config, args.api, args.desc)}:config{args.config}:{n}"
-        traffic = load_traffic(args.pmc, key)
+        kern = dispatched_kernel(args.config, args.api, w)
+        traffic, traffic_src = load_traffic(args.pmc, key, kern)
         result = {
             "metric": metric_name(),
             "value": round(value, 3),
@@ -513,12 +546,13 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": kernel_name(args.config, args.api, args.desc),
+                "kernel": kern,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": w["bytes"],
                 "kernel_ms_mean": round(float(kms.mean()), 5),
                 "kernel_ms_min": round(float(kms.min()), 5),
