@@ -22,10 +22,10 @@
 //    lowest first chunk) plus a 32-bit lane offset: `global_load_dwordx4 v,
 //    voff, s[base]`, one v_min per slot for the clamp to the last chunk.  A
 //    wave whose packets lie 4 GiB apart takes per-lane 64-bit addresses.
-//  * Masks.  One ds_read_b128 from the 17 x 17 LDS table per chunk slot; a
-//    slot that every packet of the wave covers whole (slot 1 of a 1500-B
-//    packet) skips the table and the ANDs.  The table is copied from a
-//    constant image in global memory instead of being computed per block.
+//  * Masks.  A chunk slot's mask comes from a 34-entry LDS table (bytes
+//    [0, e) and [s, 16), ANDed for the head lane); a slot that every packet
+//    of the wave covers whole (slot 1 of a 1500-B packet) skips the table and
+//    the ANDs.  The table is copied from a constant image in global memory.
 //  * Sums.  Each chunk is 4 v_dot2_u32_u16 against (1, 1) into a 32-bit
 //    lane partial (< 2^21, no fold before the reduction).
 //  * Reduction, two steps at once.  A group's partials of packet A (step k)
@@ -50,25 +50,29 @@ namespace {
 
 constexpr int kU = 3;  // chunk loads per lane and packet in one round
 
-// The 17 x 17 chunk-mask table (entry s * 17 + e keeps bytes [s, e) of a
-// 16-byte chunk) as a constant image: a block copies it into LDS with one
-// 16-byte load per thread instead of computing it (~30 VALU per entry).
-struct alignas(16) MaskWords {
-  uint32_t w[17 * 17 * 4];
+// The chunk masks as two 17-entry rows, a constant image that a block copies
+// into LDS (instead of computing ~30 VALU per entry): entry e keeps bytes
+// [0, e) of a 16-byte chunk, entry 17 + s keeps bytes [s, 16); the mask of
+// [s, e) is their AND.  A block copies 544 B; the 17 x 17 table of every
+// (s, e) cost 4.6 KB per block, and at 512 blocks per CU ~600 MB of L2 reads
+// per launch from the same lines (config 2 3.8 % slower, profiles/r03/r03s/).
+struct alignas(16) SplitWords {
+  uint32_t w[34 * 4];
 };
-constexpr MaskWords make_mask_words() {
-  MaskWords t{};
-  for (int s = 0; s < 17; ++s)
-    for (int e = 0; e < 17; ++e)
-      for (int d = 0; d < 4; ++d) {
-        uint32_t m = 0;
-        for (int b = 0; b < 4; ++b)
-          if (4 * d + b >= s && 4 * d + b < e) m |= 0xffu << (8 * b);
-        t.w[(s * 17 + e) * 4 + d] = m;
+constexpr SplitWords make_split_words() {
+  SplitWords t{};
+  for (int i = 0; i < 34; ++i)
+    for (int d = 0; d < 4; ++d) {
+      uint32_t m = 0;
+      for (int b = 0; b < 4; ++b) {
+        const int byte = 4 * d + b;
+        if (i < 17 ? byte < i : byte >= i - 17) m |= 0xffu << (8 * b);
       }
+      t.w[i * 4 + d] = m;
+    }
   return t;
 }
-__device__ const MaskWords g_mask_words = make_mask_words();
+__device__ const SplitWords g_split_words = make_split_words();
 
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 // A wave-uniform value the compiler may not reason about (keeps 32-bit
@@ -149,10 +153,18 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   constexpr uint32_t kGroups = kBlock / G;
   constexpr uint32_t kRound = 16u * G * kU;  // bytes of a span one round covers
   constexpr uint32_t kBias = 0x80000000u;    // lane offsets are biased: pairs may lie either way
-  __shared__ MaskLut lut;
+  // The split mask table (g_split_words): T[e] keeps bytes [0, e), T[17 + s]
+  // bytes [s, 16).  The 17 x 17 table it replaced cost 4 % on config 2 at
+  // 512 blocks per CU: every block copied 4.6 KB from the same L2 lines
+  // (profiles/r03/r03s/).
+  __shared__ u32x4 lut_m[34];
   // the table entry at byte address a (= 16 x entry index)
   auto lut_at = [&](uint32_t a) -> u32x4 {
-    return *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(lut.m) + a);
+    return *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(lut_m) + a);
+  };
+  // bytes [s, e) of a chunk, s and e clamped to [0, 16]
+  auto mask_se = [&](int s_, int e_) -> u32x4 {
+    return lut_m[clampi(e_, 0, 16)] & lut_m[17 + clampi(s_, 0, 16)];
   };
 
   const uint32_t lane = threadIdx.x & 63;
@@ -311,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const uint32_t k = rb + 16u * u * G;
-        r = dot_acc_masked(w[u], lut.m[MaskLut::index((int)(h0 - k), (int)(e0 - k))], r);
+        r = dot_acc_masked(w[u], mask_se((int)(h0 - k), (int)(e0 - k)), r);
       }
       acc = fold16_32(acc) + r;
     }
@@ -320,19 +332,22 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
 
   // The lane partial of one step: round 0 from registers, later rounds
   // (spans longer than kRound) serially.  Mask-table addresses are 16 x the
-  // entry index: 272 x head + 16 x clamp(end - chunk start, 0, 16).
+  // entry index: 16 x clamp(end - chunk start, 0, 16), and for the head lane
+  // 272 + 16 x head.
   auto sum_step = [&](uint32_t q0, const Geo<kP>& z, const u32x4 (&v)[kU]) -> uint32_t {
     if (z.far) return far_sum(q0, z);  // wave-uniform, rare
     uint32_t E[kP], H[kP], emin = z.e[0], emax = z.e[0];
 #pragma unroll
     for (int g = 0; g < kP; ++g) {
       E[g] = 16u * min(z.e[g], 1u << 20);  // round 0 cannot tell 2^20 from more
-      H[g] = 272u * z.h[g];
+      H[g] = 16u * z.h[g];
       emin = min(emin, z.e[g]);
       emax = max(emax, z.e[g]);
     }
     const uint32_t e16 = gsel(E) + negpos16;
-    uint32_t acc = dot_acc_masked(v[0], lut_at((gsel(H) & m0) + clampi((int)e16, 0, 256)), 0u);
+    // head lane: T[e] & T[17 + h]; the others: T[e] & T[17] (all ones)
+    const u32x4 m = lut_at(clampi((int)e16, 0, 256)) & lut_at(272u + (gsel(H) & m0));
+    uint32_t acc = dot_acc_masked(v[0], m, 0u);
 #pragma unroll
     for (int u = 1; u < kU; ++u) {
       if (emin >= 16u * (u + 1) * G)  // wave-uniform: every lane's chunk is whole
@@ -350,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
         uint32_t r = 0;
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-          r = dot_acc_masked(x[u], lut.m[clampi((int)(e0 - rb - 16u * u * G), 0, 16)], r);
+          r = dot_acc_masked(x[u], lut_m[clampi((int)(e0 - rb - 16u * u * G), 0, 16)], r);
         acc = fold16_32(acc) + r;  // < 2^21: 64 lanes of it still fit 32 bits
       }
     }
@@ -414,19 +429,10 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   // The block's mask table: its words are loaded first (L2 hits), then the
   // first step's chunks, and the table is written to LDS while those are in
   // flight (the wait before the writes covers only the table's loads).
-  // Computing it instead (30 VALU per entry) measured 2 % faster warm at 512
-  // blocks per CU but slower in the driver's window (0.864 / 0.869 against
-  // 0.889 / 0.872, profiles/r03/r03m/); 1024-thread blocks were no better at
-  // 128 per CU and 13 % slower at 512 (r03l/).
-  const u32x4* lsrc = reinterpret_cast<const u32x4*>(g_mask_words.w);
-  const u32x4 lw0 = lsrc[threadIdx.x];
-  const u32x4 lw1 = lsrc[min(threadIdx.x + kBlock, 17u * 17u - 1u)];
+  const uint32_t li = min(threadIdx.x, 33u);
+  const u32x4 lw0 = reinterpret_cast<const u32x4*>(g_split_words.w)[li];
   zA = load_step(desc(min(q, qmax)), vA);
-  lut.m[threadIdx.x] = lw0;
-  // unconditional (threads past the table rewrite its last entry with the
-  // same word): under a branch the compiler sinks lw1's load into it and
-  // waits for every load in flight, the first step's chunks included
-  lut.m[min(threadIdx.x + kBlock, 17u * 17u - 1u)] = lw1;
+  lut_m[li] = lw0;  // unconditional: threads past the table rewrite its last entry
   __syncthreads();  // every thread reaches this barrier: no exit before it
   if (q >= n) return;  // wave-uniform
   const uint32_t K = (n - q + S - 1) / S;  // live steps of this wave, >= 1
@@ -485,7 +491,10 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
     uint32_t remap, uint64_t stride, uint32_t slen) {
   constexpr uint32_t kRoundB = 64u * U;  // bytes of a span one round covers
   constexpr uint32_t kWavesPB = kBlock / 64;
-  __shared__ MaskLut lut;
+  __shared__ u32x4 lut_m[34];  // the split mask table (see k_spans_lean)
+  auto mask_se = [&](int s_, int e_) -> u32x4 {
+    return lut_m[clampi(e_, 0, 16)] & lut_m[17 + clampi(s_, 0, 16)];
+  };
   const uint32_t lane = threadIdx.x & 63, gi = lane >> 2, gl = lane & 3;
   const __amdgpu_buffer_rsrc_t out_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(2u * n), 0x00020000);
@@ -569,7 +578,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
       if (__ballot(!(s <= 0 && e >= 16)) == 0)  // wave-uniform: every chunk whole
         acc = dot_acc(v[u], acc);
       else if (__ballot(e > 0) != 0)  // some lane holds bytes of this slot
-        acc = dot_acc_masked(v[u], lut.m[MaskLut::index(s, e)], acc);
+        acc = dot_acc_masked(v[u], mask_se(s, e), acc);
     }
     if (__ballot(z.e > kRoundB)) pend |= 1u << j;  // wave-uniform
     return acc;
@@ -582,7 +591,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
       const uint32_t cb = rb + 16u * gl;
       const u32x4 w = load_chunk(y.c0 + min(cb, y.lb));
       acc = fold16_32(acc) +
-            dot_acc_masked(w, lut.m[MaskLut::index((int)(y.h - cb), (int)(y.e - cb))], 0u);
+            dot_acc_masked(w, mask_se((int)(y.h - cb), (int)(y.e - cb)), 0u);
     }
     return acc;
   };
@@ -623,9 +632,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
   };
 
   // the mask table: its words first (L2 hits), then the first step
-  const u32x4* lsrc = reinterpret_cast<const u32x4*>(g_mask_words.w);
-  const u32x4 lw0 = lsrc[threadIdx.x];
-  const u32x4 lw1 = lsrc[min(threadIdx.x + kBlock, 17u * 17u - 1u)];
+  const u32x4 lw0 = reinterpret_cast<const u32x4*>(g_split_words.w)[min(threadIdx.x, 33u)];
   // super-steps of 64 packets; wave w takes super-steps w, w + NW, ... (the
   // host keeps n + 2 S below 2^32)
   const uint32_t NW = gridDim.x * kWavesPB;
@@ -641,11 +648,10 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
   B b1 = blk(min(p + S, n - 1));
   zA = geo(b0, p, 0);
   load(zA, vA);
-  lut.m[threadIdx.x] = lw0;
   // unconditional (threads past the table rewrite its last entry with the
-  // same word): under a branch the compiler sinks lw1's load into it and waits
+  // same word): under a branch the compiler sinks the load into it and waits
   // for every load in flight, the first step's chunks included
-  lut.m[min(threadIdx.x + kBlock, 17u * 17u - 1u)] = lw1;
+  lut_m[min(threadIdx.x, 33u)] = lw0;
   __syncthreads();  // every thread reaches this barrier: no exit before it
   if (p >= n) return;  // wave-uniform
   // The four steps of a full super-step at p (step 0 in flight in A), the

@@ -15,8 +15,9 @@ for spec in ${CONFIGS:-2 3 3tx 5 5tso}; do
   step bench_$t 600 python3 bench.py --config $c --api $api
   step trace_$t 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$t" -o run --output-format csv -- python3 bench.py --config $c --api $api --cpu-baseline off
   step pmc_$t 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$t" -o run --output-format csv -- python3 bench.py --config $c --api $api --steps 10 --warmup 2 --cpu-baseline off
-  read B N K <<<"$(python3 -c "import json; d=json.loads([l for l in open('$OUT/bench_$t.log') if l.startswith('{')][-1]); print(d['config']['algorithmic_bytes_per_gpu'], d['config']['packets_per_gpu'], d['roofline']['kernel'])")"
-  python3 tools/pmc_summary.py "$OUT/pmc_$t" --key "$K:config$c:$N" --bytes "$B" --out profiles/pmc_traffic.json > "$OUT/pmc_$t.summary.json"
+  # the key the bench looks its traffic up by (roofline.traffic_source.key)
+  read B KEY <<<"$(python3 -c "import json; d=json.loads([l for l in open('$OUT/bench_$t.log') if l.startswith('{')][-1]); print(d['config']['algorithmic_bytes_per_gpu'], d['roofline']['traffic_source']['key'])")"
+  python3 tools/pmc_summary.py "$OUT/pmc_$t" --key "$KEY" --bytes "$B" --out profiles/pmc_traffic.json > "$OUT/pmc_$t.summary.json"
   python3 tools/pmc_summary.py "$OUT/trace_$t" > "$OUT/trace_$t.summary.json"
 done
 cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json"
