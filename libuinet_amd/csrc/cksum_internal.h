@@ -46,7 +46,8 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
 int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const uint32_t* seed,
                    uint16_t* out, uint32_t n, uint32_t flags, hipStream_t stream);
 // k_spans_lean (cksum_spans.hip): G = 32 or 64 lanes per packet; strided
-// takes packet i at base + i * stride, slen bytes (off / len unused).
+// takes packet i at base + i * stride, slen bytes (off / len unused);
+// blocks_cu 0 = two steps per wave, else at most blocks_cu blocks per CU.
 int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,

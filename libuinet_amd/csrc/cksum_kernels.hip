@@ -368,7 +368,7 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   const bool sdesc = tuning().spans_sdesc && geo.g >= 32;
   if (sdesc && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, false, 0, 0,
-                             blocks_per_cu(256), stream);
+                             tuning().blocks_per_cu, stream);
   if (sdesc && pipe) {
     const int grid = grid_for(n, geo.g, 128);
 #define LP(G, U)                                                                          \
@@ -418,7 +418,7 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
                              pkt_stride, len, blocks_per_cu(128), stream);
   if (geo.g >= 32 && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, nullptr, nullptr, seed, nullptr, out, n, flags, geo.g, true,
-                             pkt_stride, len, blocks_per_cu(256), stream);
+                             pkt_stride, len, tuning().blocks_per_cu, stream);
   if (geo.g >= 32 && pipe) {
     // the persistent two-in-flight groups of k_spans_pp, descriptors from
     // the stride: as for the span API, the one-shot grid (spans_pipe = 0)

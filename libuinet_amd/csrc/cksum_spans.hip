@@ -359,14 +359,35 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
       Geo<kP> z2;
       const Addr w = addr(desc(q0), z2);
       const uint32_t e0 = gsel(z.e) - pos0;
-      for (uint32_t rb = kRound; rb < emax; rb += kRound) {
-        u32x4 x[kU];
-        load_round(w, rb, x);
+      auto round_sum = [&](const u32x4 (&x)[kU], uint32_t rb) {
         uint32_t r = 0;
 #pragma unroll
         for (int u = 0; u < kU; ++u)
           r = dot_acc_masked(x[u], lut_m[clampi((int)(e0 - rb - 16u * u * G), 0, 16)], r);
         acc = fold16_32(acc) + r;  // < 2^21: 64 lanes of it still fit 32 bits
+      };
+      if constexpr (kP == 1) {
+        // one packet per wave (9000-B frames: three 3-KB rounds): round i + 1
+        // loads while round i is summed, two register sets in turn; a round
+        // past the end re-reads the span's last chunk (never loaded under a
+        // branch, so the wait for round i leaves round i + 1 in flight)
+        const uint32_t nr = (emax - 1) / kRound;  // rounds after round 0, >= 1
+        u32x4 x[kU], y[kU];
+        load_round(w, kRound, x);
+        for (uint32_t i = 1;; i += 2) {
+          load_round(w, (i + 1) * kRound, y);
+          round_sum(x, i * kRound);
+          if (i + 1 > nr) break;
+          load_round(w, (i + 2) * kRound, x);
+          round_sum(y, (i + 1) * kRound);
+          if (i + 2 > nr) break;
+        }
+      } else {
+        for (uint32_t rb = kRound; rb < emax; rb += kRound) {
+          u32x4 x[kU];
+          load_round(w, rb, x);
+          round_sum(x, rb);
+        }
       }
     }
     return acc;
@@ -763,9 +784,19 @@ int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len
                       uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream) {
   const uint32_t groups = kBlock / g;
-  uint64_t blocks = ((uint64_t)n + groups - 1) / groups;
+  // Two steps per wave by default at 32 lanes per packet (2 x 1500 B each):
+  // config 2 at 2 steps (256 blocks per CU) is flat through the driver's
+  // window and within 4 % of the widest grid warm; 4 steps lost 3-4 % warm
+  // (configs 2 and 4), 1 step ramps after an idle gap (profiles/r03/r03t/,
+  // r03z/).  At 64 lanes a step is one packet of >= 1.5 KB (9 KB in config
+  // 5, where 2 steps per wave lost 1.2 %): one step per wave.  blocks_cu > 0
+  // (the knob) caps the grid at blocks_cu per CU instead.
+  const uint64_t spw = g == 32 ? 2 : 1;  // steps per wave
+  uint64_t blocks = ((uint64_t)n + spw * groups - 1) / (spw * groups);
+  const uint64_t lim = blocks_cu > 0 ? 256ull * (uint64_t)blocks_cu : 256ull * 4096ull;
   // the kernel's 32-bit packet indices need n + 3 * blocks * groups < 2^32
-  const uint64_t cap = std::min<uint64_t>(256ull * (uint64_t)blocks_cu, (1ull << 26) / groups);
+  const uint64_t cap = std::min<uint64_t>(lim, (1ull << 26) / groups);
+  if (blocks_cu > 0) blocks = ((uint64_t)n + groups - 1) / groups;
   blocks = std::max<uint64_t>(1, std::min(blocks, cap));
   const dim3 grid((uint32_t)blocks), blk(kBlock);
   const uint8_t* b = static_cast<const uint8_t*>(base);
