@@ -107,6 +107,40 @@ def test_in_cksum_update_inline(tmp_path):
         assert _ip_fold(bytes(buf)) == 0xFFFF
 
 
+def test_in_cksum_update_matches_reference(tmp_path):
+    """include/uinet_cksum.h's in_cksum_update against the reference's own
+    (machine/in_cksum.h:46-72, compiled into oracle/_ref by oracle/Makefile as
+    ref_in_cksum_update): every ip_sum value and 2000 random headers give the
+    same 20 bytes."""
+    import ctypes
+
+    import oracle
+
+    if not oracle.have_reference():
+        pytest.skip("oracle/_ref/libref_cksum.so not built (needs /root/reference)")
+    ref = ctypes.CDLL(oracle.REF_SO)
+    if not hasattr(ref, "ref_in_cksum_update"):
+        pytest.skip("oracle/_ref predates ref_in_cksum_update: run `make -C oracle ref`")
+    ref.ref_in_cksum_update.argtypes = [ctypes.c_void_p]
+    src = tmp_path / "upd.c"
+    src.write_text('#include "uinet_cksum.h"\nvoid upd(void *h) { uinet_in_cksum_update(h); }\n')
+    so = tmp_path / "upd.so"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-shared", "-fPIC",
+                    "-I", os.path.join(REPO, "include"), "-o", str(so), str(src)], check=True)
+    upd = ctypes.CDLL(str(so)).upd
+    upd.argtypes = [ctypes.c_void_p]
+    ours, theirs = (ctypes.c_uint8 * 20)(), (ctypes.c_uint8 * 20)()
+    rng = np.random.default_rng(12)
+    hdrs = [bytes([0x45, 0] + [0] * 8 + [s >> 8, s & 0xFF] + [0] * 8) for s in range(0x10000)]
+    hdrs += [rng.integers(0, 256, 20, dtype=np.uint8).tobytes() for _ in range(2000)]
+    for h in hdrs:
+        ctypes.memmove(ours, h, 20)
+        ctypes.memmove(theirs, h, 20)
+        upd(ours)
+        ref.ref_in_cksum_update(theirs)
+        assert bytes(ours) == bytes(theirs), h.hex()
+
+
 @pytest.mark.parametrize("order", ["reference_first", "opt_out_macro", "ours_only"])
 def test_in_cksum_update_include_order(tmp_path, order):
     """The reference-named in_cksum_update shim next to a reference-style
