@@ -56,8 +56,8 @@ def parse():
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU")
     ap.add_argument("--api", choices=["spans", "strided"], default="spans")
     ap.add_argument("--desc", choices=["wide", "packed"], default="wide",
-                    help="chain configs: 12-B (uinet_cksum_chains) or packed 6-B "
-                    "(uinet_cksum_chains32) segment descriptors")
+                    help="12-B wide (uinet_cksum_chains / uinet_cksum_spans) or packed "
+                    "6-B (uinet_cksum_chains32 / uinet_cksum_spans32) descriptors")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
@@ -169,14 +169,17 @@ def make_launch(cfg: str, w, api: str, out, desc: str = "wide"):
         base = w["arena"][w["base"]:]
         return lambda s: u.cksum_strided(base, w["stride"], w["length"], w["n"], out=out, stream=s)
     seed = w.get("seed")
-    return lambda s: u.cksum_spans(w["arena"], w["off"], w["len"], seed=seed, out=out,
+    off, ln = (w["off"], w["len"]) if desc == "wide" else w["packed"]
+    return lambda s: u.cksum_spans(w["arena"], off, ln, seed=seed, out=out,
                                    len_hint=w["hint"], stream=s)
 
 
 def kernel_name(cfg: str, api: str, desc: str = "wide") -> str:
     if cfg in CHAIN_CONFIGS:
         return "k_chains32" if desc == "packed" else "k_chains"
-    return "k_strided" if api == "strided" else "k_spans"
+    if api == "strided":
+        return "k_strided"
+    return "k_spans32" if desc == "packed" else "k_spans"
 
 
 def dispatched_kernel(cfg: str, api: str, w) -> str:
@@ -446,6 +449,8 @@ def main():
         torch.cuda.set_stream(stream)
     if args.desc == "packed" and args.config in CHAIN_CONFIGS:
         w["packed"] = u.pack_segments(w["seg_off"], w["seg_len"])
+    elif args.desc == "packed" and args.api == "spans":
+        w["packed"] = u.pack_segments(w["off"], w["len"])
     launches = [make_launch(args.config, w, args.api, o, args.desc) for o in outs]
     counts = [n] * world
     rg = ResultGather(counts, "cuda", depth=NBUF) if distributed else None
@@ -536,7 +541,8 @@ def main():
                 "workload": w["desc"],
                 "packets_per_gpu": n,
                 "algorithmic_bytes_per_gpu": w["bytes"],
-                "api": {"spans": "uinet_cksum_spans", "strided": "uinet_cksum_strided"}[args.api]
+                "api": {"spans": "uinet_cksum_spans" + ("32" if args.desc == "packed" else ""),
+                        "strided": "uinet_cksum_strided"}[args.api]
                 if args.config not in CHAIN_CONFIGS else
                 {"wide": "uinet_cksum_chains", "packed": "uinet_cksum_chains32"}[args.desc],
                 "parallelism": f"dp{world} packet shards" + (

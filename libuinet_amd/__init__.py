@@ -46,8 +46,8 @@ OK, EINVAL, ENODEV, ENOMEM, EHIP = 0, -22, -19, -12, -5
 EXPORTED_SYMBOLS = (
     "in_cksum_skip", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo", "in_addword",
     "uinet_cksum_version", "uinet_cksum_strerror", "uinet_cksum_last_hip_error",
-    "uinet_cksum_device_ok", "uinet_cksum_set_tuning", "uinet_cksum_spans", "uinet_cksum_strided", "uinet_cksum_chains",
-    "uinet_cksum_chains32",
+    "uinet_cksum_device_ok", "uinet_cksum_set_tuning", "uinet_cksum_spans", "uinet_cksum_spans32",
+    "uinet_cksum_strided", "uinet_cksum_chains", "uinet_cksum_chains32",
     "in_cksum_skip_batch", "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch",
     "uinet_cksum_register_host", "uinet_cksum_unregister_host",
     "uinet_cksum_rx_offload", "uinet_cksum_tx_offload",
@@ -101,6 +101,7 @@ def lib() -> ctypes.CDLL:
         "uinet_cksum_device_ok": (_i32, []),
         "uinet_cksum_set_tuning": (_i32, [ctypes.c_char_p, _i32]),
         "uinet_cksum_spans": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]),
+        "uinet_cksum_spans32": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]),
         "uinet_cksum_strided": (_i32, [_vp, _u64, _u32, _vp, _vp, _u32, _u32, _vp]),
         "uinet_cksum_chains": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32,
                                        _vp]),
@@ -293,20 +294,31 @@ def _out(n, out, like):
 def cksum_spans(base, off, length, seed=None, parity=None, out=None, flags: int = 0,
                 len_hint: int = 0, stream=None):
     """out[i] = checksum of ``base[off[i] : off[i] + length[i]]`` (device u8 tensor
-    ``base``; int64 ``off``; int32 ``length``; optional uint32-valued int32
-    ``seed``; optional uint8 ``parity``)."""
+    ``base``; optional uint32-valued int32 ``seed``; optional uint8 ``parity``).
+    Wide descriptors (int64 ``off``, int32 ``length``) call uinet_cksum_spans;
+    packed ones (uint32-valued int32 ``off``, uint16 or uint16-valued int16
+    ``length``: arenas < 4 GiB, spans <= 65535 B; see :func:`pack_segments`)
+    call uinet_cksum_spans32."""
     import torch
 
     _dev(base, torch.uint8, "base")
-    _dev(off, torch.int64, "off")
-    _dev(length, torch.int32, "length")
+    packed = off is not None and off.dtype == torch.int32
+    if packed:
+        _dev(off, torch.int32, "off")
+        if length is not None and length.dtype == torch.uint16:
+            length = length.view(torch.int16)
+        _dev(length, torch.int16, "length")
+    else:
+        _dev(off, torch.int64, "off")
+        _dev(length, torch.int32, "length")
     _dev(seed, torch.int32, "seed")
     _dev(parity, torch.uint8, "parity")
     n = off.numel()
     if length.numel() != n:
         raise ValueError("off/length size mismatch")
     out = _out(n, out, base)
-    _check("uinet_cksum_spans", lib().uinet_cksum_spans(
+    fn = "uinet_cksum_spans32" if packed else "uinet_cksum_spans"
+    _check(fn, getattr(lib(), fn)(
         _dp(base), _dp(off), _dp(length), _dp(seed), _dp(parity), _dp(out), n, flags,
         len_hint, _stream(stream)))
     return out
@@ -362,8 +374,9 @@ def cksum_chains(base, seg_off, seg_len, pkt_seg, length=None, skip=None, seed=N
 
 
 def pack_segments(seg_off, seg_len):
-    """Wide chain descriptors (int64 offsets, int32 lengths; numpy or torch) to
-    the packed form of uinet_cksum_chains32: int32 holding the uint32 offset,
+    """Wide chain or span descriptors (int64 offsets, int32 lengths; numpy or
+    torch) to the packed form of uinet_cksum_chains32 / uinet_cksum_spans32:
+    int32 holding the uint32 offset,
     int16 holding the uint16 length.  Raises ValueError when an offset is not
     below 4 GiB or a length exceeds 65535, instead of truncating."""
     if hasattr(seg_off, "cpu"):

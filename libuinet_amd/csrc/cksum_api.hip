@@ -921,6 +921,16 @@ int uinet_cksum_spans(const void* base, const uint64_t* off, const uint32_t* len
                       static_cast<hipStream_t>(stream));
 }
 
+int uinet_cksum_spans32(const void* base, const uint32_t* off, const uint16_t* len,
+                        const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                        uint32_t flags, uint32_t len_hint, void* stream) {
+  if (n == 0) return UINET_CKSUM_OK;
+  if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
+  if (!base || !off || !len || !out) return UINET_CKSUM_EINVAL;
+  return launch_spans32(base, off, len, seed, parity, out, n, flags, len_hint,
+                        static_cast<hipStream_t>(stream));
+}
+
 int uinet_cksum_strided(const void* base, uint64_t stride, uint32_t len, const uint32_t* seed,
                         uint16_t* out, uint32_t n, uint32_t flags, void* stream) {
   if (n == 0) return UINET_CKSUM_OK;

@@ -45,16 +45,24 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
                  uint32_t flags, uint32_t len_hint, hipStream_t stream);
 int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const uint32_t* seed,
                    uint16_t* out, uint32_t n, uint32_t flags, hipStream_t stream);
+// Packed span descriptors (uinet_cksum_spans32): u32 offsets, u16 lengths.
+int launch_spans32(const void* base, const uint32_t* off, const uint16_t* len,
+                   const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                   uint32_t flags, uint32_t len_hint, hipStream_t stream);
 // k_spans_lean (cksum_spans.hip): G = 32 or 64 lanes per packet; strided
-// takes packet i at base + i * stride, slen bytes (off / len unused);
-// blocks_cu 0 = two steps per wave, else at most blocks_cu blocks per CU.
-int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len,
+// takes packet i at base + i * stride, slen bytes (off / len unused, wide
+// descriptor types only); blocks_cu 0 = two steps per wave, else at most
+// blocks_cu blocks per CU.  Instantiated for (uint64_t, uint32_t) and
+// (uint32_t, uint16_t) descriptors.
+template <typename OffT, typename LenT>
+int launch_spans_lean(const void* base, const OffT* off, const LenT* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream);
 // k_spans_quad (cksum_spans.hip): 4 lanes per packet, U = 1 or 2 chunk
-// slots per lane, for small packets.
-int launch_spans_quad(const void* base, const uint64_t* off, const uint32_t* len,
+// slots per lane, for small packets.  Same instantiations.
+template <typename OffT, typename LenT>
+int launch_spans_quad(const void* base, const OffT* off, const LenT* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int u, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream);

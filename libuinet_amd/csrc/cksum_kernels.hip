@@ -39,15 +39,25 @@ __device__ __forceinline__ uint64_t sload64(const uint64_t* p) {
 __device__ __forceinline__ uint32_t sload32(const uint32_t* p) {
   return *(const __attribute__((address_space(4))) uint32_t*)(uintptr_t)p;
 }
+// Span descriptors, wide (u64 offset, u32 length) or packed (u32 offset,
+// u16 length: uinet_cksum_spans32; a u16 comes from the aligned dword that
+// holds it).
+__device__ __forceinline__ uint64_t sload_off(const uint64_t* p) { return sload64(p); }
+__device__ __forceinline__ uint64_t sload_off(const uint32_t* p) { return sload32(p); }
+__device__ __forceinline__ uint32_t sload_len(const uint32_t* p) { return sload32(p); }
+__device__ __forceinline__ uint32_t sload_len(const uint16_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return (sload32(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)) >> (8 * (a & 2))) & 0xffffu;
+}
 
 // The descriptors of packet p for lane group `gi` of a wave whose kP = 64 / G
 // groups own the consecutive packets p - gi .. p - gi + kP - 1: kP scalar
 // loads of off / len (clamped to n - 1), then a per-lane select.  Without
 // it every group's off[p] / len[p] is a vector load of its own, 2 of the 5
 // vector-memory instructions per wave and packet pair at 1500 B.
-template <int G>
-__device__ __forceinline__ void wave_desc(const uint64_t* __restrict__ off,
-                                          const uint32_t* __restrict__ len, uint32_t p, uint32_t n,
+template <int G, typename OffT, typename LenT>
+__device__ __forceinline__ void wave_desc(const OffT* __restrict__ off,
+                                          const LenT* __restrict__ len, uint32_t p, uint32_t n,
                                           uint64_t& o, uint32_t& l) {
   constexpr int kP = 64 / G;
   const uint32_t gi = (threadIdx.x & 63) / G;
@@ -59,10 +69,10 @@ __device__ __forceinline__ void wave_desc(const uint64_t* __restrict__ off,
     const uint32_t q = min(p0 + (uint32_t)k, n - 1);
     // readfirstlane keeps each value scalar: without it the compiler folds
     // the select of kP loads back into one per-lane (vector) load of off[p]
-    const uint64_t o64 = sload64(off + q);
+    const uint64_t o64 = sload_off(off + q);
     const uint64_t ok = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o64 >> 32)) << 32) |
                         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)o64);
-    const uint32_t lk = __builtin_amdgcn_readfirstlane(sload32(len + q));
+    const uint32_t lk = __builtin_amdgcn_readfirstlane(sload_len(len + q));
     if (gi == (uint32_t)k) {
       o = ok;
       l = lk;
@@ -86,10 +96,11 @@ __device__ __forceinline__ uint32_t wave_u32(const uint32_t* __restrict__ a, uin
   return r;
 }
 
-template <int G, int U, bool kStrided, bool kSDesc = false>
+template <int G, int U, bool kStrided, bool kSDesc = false, typename OffT = uint64_t,
+          typename LenT = uint32_t>
 __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ base,
-                                                 const uint64_t* __restrict__ off,
-                                                 const uint32_t* __restrict__ len,
+                                                 const OffT* __restrict__ off,
+                                                 const LenT* __restrict__ len,
                                                  const uint32_t* __restrict__ seed,
                                                  const uint8_t* __restrict__ parity,
                                                  uint64_t pkt_stride, uint32_t fixed_len,
@@ -111,8 +122,8 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
     wave_desc<G>(off, len, p, n, o, l);
     if (!live) l = 0;
   } else if (live) {
-    o = kStrided ? (uint64_t)p * pkt_stride : off[p];
-    l = kStrided ? fixed_len : len[p];
+    o = kStrided ? (uint64_t)p * pkt_stride : (uint64_t)off[p];
+    l = kStrided ? fixed_len : (uint32_t)len[p];
   }
   const uint8_t* a = base + o;
   Span<G, U> sp;
@@ -130,8 +141,8 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
     if constexpr (kSDesc && !kStrided) {
       wave_desc<G>(off, len, pn, n, on, ln);
     } else {
-      on = kStrided ? (uint64_t)pc * pkt_stride : off[pc];
-      ln = kStrided ? fixed_len : len[pc];
+      on = kStrided ? (uint64_t)pc * pkt_stride : (uint64_t)off[pc];
+      ln = kStrided ? fixed_len : (uint32_t)len[pc];
     }
     // a span of one round folds its 32-bit sum (< U * 2^19) directly
     const uint32_t a0 = l ? sp.sum_lut_first(lut, gl) : 0u;
@@ -350,12 +361,41 @@ int blocks_per_cu(int dflt) {
 //   0 k_spans: one packet per lane group, one-shot grid.
 // Geometries other than 32 x 3 / 64 x 3 (the spans_geo override) use k_spans_pp
 // under 1 and 2.
-int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
-                 const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
-                 uint32_t flags, uint32_t len_hint, hipStream_t stream) {
+// k_spans_pp at G x U (spans_pipe 2, wide descriptors only).
+static int launch_spans_pp(const void* base, const uint64_t* off, const uint32_t* len,
+                           const uint32_t* seed, const uint8_t* parity, uint16_t* out,
+                           uint32_t n, uint32_t flags, Geometry geo, hipStream_t stream) {
+  const int grid = grid_for(n, geo.g, 128);
+#define LP(G, U)                                                                          \
+  if (parity)                                                                             \
+    hipLaunchKernelGGL((k_spans_pp<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,      \
+                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
+                       flags, (uint32_t)tuning().xcd_remap);                               \
+  else                                                                                    \
+    hipLaunchKernelGGL((k_spans_pp<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,     \
+                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
+                       flags, (uint32_t)tuning().xcd_remap)
+  switch (geo.g * 16 + geo.u) {
+    case 32 * 16 + 3: LP(32, 3); break;
+    case 64 * 16 + 2: LP(64, 2); break;
+    default: LP(64, 3); break;
+  }
+#undef LP
+  return check_launch();
+}
+
+// Packed descriptors (uinet_cksum_spans32) take the same kernels; under
+// spans_pipe 2 (k_spans_pp, an A/B knob built for wide descriptors only) they
+// take the one-shot k_spans of spans_pipe 0.
+template <typename OffT, typename LenT>
+static int launch_spans_t(const void* base, const OffT* off, const LenT* len,
+                          const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                          uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
+  constexpr bool kWide = sizeof(OffT) == 8;
   const Geometry geo = geometry_override(pick_geometry(len_hint));
-  const int pipe = tuning().spans_pipe;
+  int pipe = tuning().spans_pipe;
+  if (!kWide && pipe == 2) pipe = 0;
   // Scalar descriptors (G >= 32, knob "spans_sdesc", default on): a wave's
   // 1-2 packets' off / len come from s_loads, and the grid drops to one packet
   // per group (512 blocks per CU at 1 M x 1500 B).  Interleaved A/B, config 2
@@ -369,38 +409,35 @@ int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
   if (sdesc && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, false, 0, 0,
                              tuning().blocks_per_cu, stream);
-  if (sdesc && pipe) {
-    const int grid = grid_for(n, geo.g, 128);
-#define LP(G, U)                                                                          \
-  if (parity)                                                                             \
-    hipLaunchKernelGGL((k_spans_pp<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,      \
-                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
-                       flags, (uint32_t)tuning().xcd_remap);                               \
-  else                                                                                    \
-    hipLaunchKernelGGL((k_spans_pp<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,     \
-                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
-                       flags, (uint32_t)tuning().xcd_remap)
-    switch (geo.g * 16 + geo.u) {
-      case 32 * 16 + 3: LP(32, 3); break;
-      case 64 * 16 + 2: LP(64, 2); break;
-      default: LP(64, 3); break;
-    }
-#undef LP
-    return check_launch();
+  if constexpr (kWide) {
+    if (sdesc && pipe) return launch_spans_pp(base, off, len, seed, parity, out, n, flags, geo,
+                                              stream);
   }
   const int grid = grid_for(n, geo.g, sdesc ? 512 : 256);
 #define L(G, U)                                                                          \
   if (sdesc && (G) >= 32)                                                                \
-    hipLaunchKernelGGL((k_spans<G, U, false, true>), dim3(grid), dim3(kBlock), 0, stream, \
-                       static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
-                       out, n, flags, (uint32_t)tuning().xcd_remap);                     \
+    hipLaunchKernelGGL((k_spans<G, U, false, true, OffT, LenT>), dim3(grid), dim3(kBlock), \
+                       0, stream, static_cast<const uint8_t*>(base), off, len, seed, parity, \
+                       0ull, 0u, out, n, flags, (uint32_t)tuning().xcd_remap);           \
   else                                                                                   \
-    hipLaunchKernelGGL((k_spans<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,       \
-                       static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, \
-                       out, n, flags, (uint32_t)tuning().xcd_remap)
+    hipLaunchKernelGGL((k_spans<G, U, false, false, OffT, LenT>), dim3(grid), dim3(kBlock), \
+                       0, stream, static_cast<const uint8_t*>(base), off, len, seed, parity, \
+                       0ull, 0u, out, n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
+}
+
+int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
+                 const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                 uint32_t flags, uint32_t len_hint, hipStream_t stream) {
+  return launch_spans_t(base, off, len, seed, parity, out, n, flags, len_hint, stream);
+}
+
+int launch_spans32(const void* base, const uint32_t* off, const uint16_t* len,
+                   const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
+                   uint32_t flags, uint32_t len_hint, hipStream_t stream) {
+  return launch_spans_t(base, off, len, seed, parity, out, n, flags, len_hint, stream);
 }
 
 int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const uint32_t* seed,
@@ -414,11 +451,13 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   // k_spans_quad for 16-B aligned packets of <= 64 B (one chunk per lane);
   // unaligned ones run k_spans<4, 2>, 5 % faster there (profiles/r03/r03p/)
   if (pipe == 1 && geo.g == 4 && geo.u == 1)
-    return launch_spans_quad(base, nullptr, nullptr, seed, nullptr, out, n, flags, 1, true,
-                             pkt_stride, len, blocks_per_cu(128), stream);
+    return launch_spans_quad<uint64_t, uint32_t>(base, nullptr, nullptr, seed, nullptr, out, n,
+                                                 flags, 1, true, pkt_stride, len,
+                                                 blocks_per_cu(128), stream);
   if (geo.g >= 32 && pipe == 1 && geo.u == 3)
-    return launch_spans_lean(base, nullptr, nullptr, seed, nullptr, out, n, flags, geo.g, true,
-                             pkt_stride, len, tuning().blocks_per_cu, stream);
+    return launch_spans_lean<uint64_t, uint32_t>(base, nullptr, nullptr, seed, nullptr, out, n,
+                                                 flags, geo.g, true, pkt_stride, len,
+                                                 tuning().blocks_per_cu, stream);
   if (geo.g >= 32 && pipe) {
     // the persistent two-in-flight groups of k_spans_pp, descriptors from
     // the stride: as for the span API, the one-shot grid (spans_pipe = 0)
@@ -440,7 +479,8 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
   const int grid = grid_for(n, geo.g, len <= 96 ? 256 : 4096);
 #define L(G, U)                                                                        \
-  hipLaunchKernelGGL((k_spans<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,        \
+  hipLaunchKernelGGL((k_spans<G, U, true, false, uint64_t, uint32_t>), dim3(grid),      \
+                     dim3(kBlock), 0, stream,                                          \
                      static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
                      pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)

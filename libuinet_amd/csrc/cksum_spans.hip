@@ -98,6 +98,16 @@ __device__ __forceinline__ uint32_t sld8w(const uint8_t* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   return sld32(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3));
 }
+// Span descriptors by scalar loads, wide (u64 offset, u32 length:
+// uinet_cksum_spans) or packed (u32 offset, u16 length: uinet_cksum_spans32).
+// A u16 length comes from the aligned dword that holds it.
+__device__ __forceinline__ uint64_t sld_off(const uint64_t* p) { return sld64(p); }
+__device__ __forceinline__ uint64_t sld_off(const uint32_t* p) { return sld32(p); }
+__device__ __forceinline__ uint32_t sld_len(const uint32_t* p) { return sld32(p); }
+__device__ __forceinline__ uint32_t sld_len(const uint16_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return (sld32(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)) >> (8 * (a & 2))) & 0xffffu;
+}
 
 // Four dot2 against (1, 1): both 16-bit halves of every word added into acc.
 __device__ __forceinline__ uint32_t dot_acc(u32x4 v, uint32_t acc) {
@@ -142,10 +152,10 @@ struct Geo {
   uint32_t sd[kP];  // Step::sd
 };
 
-template <int G, bool kParity, bool kSeed, bool kStrided>
+template <int G, bool kParity, bool kSeed, bool kStrided, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) void k_spans_lean(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed,
+    const uint8_t* __restrict__ base, const OffT* __restrict__ off,
+    const LenT* __restrict__ len, const uint32_t* __restrict__ seed,
     const uint8_t* __restrict__ parity, uint16_t* __restrict__ out, uint32_t n, uint32_t flags,
     uint32_t remap, uint64_t stride, uint32_t slen) {
   static_assert(G == 32 || G == 64, "one or two packets per wave");
@@ -215,8 +225,8 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
         s.o[g] = (uint64_t)qg * stride;
         s.l[g] = slen;
       } else {
-        s.o[g] = sld64(off + qg);
-        s.l[g] = sld32(len + qg);
+        s.o[g] = sld_off(off + qg);
+        s.l[g] = sld_len(len + qg);
       }
       s.sd[g] = kSeed ? sld32(seed + qg) : 0u;
       s.lp[g] = kParity ? sld8w(parity + qg) : 0u;
@@ -504,10 +514,10 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
 //    collects packet i's result of the super-step (one ds_bpermute per step)
 //    and the 64 results leave in one 128-B store (through a buffer resource:
 //    lanes past the batch address past its end).
-template <int U, bool kParity, bool kSeed, bool kStrided>
+template <int U, bool kParity, bool kSeed, bool kStrided, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) void k_spans_quad(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed,
+    const uint8_t* __restrict__ base, const OffT* __restrict__ off,
+    const LenT* __restrict__ len, const uint32_t* __restrict__ seed,
     const uint8_t* __restrict__ parity, uint16_t* __restrict__ out, uint32_t n, uint32_t flags,
     uint32_t remap, uint64_t stride, uint32_t slen) {
   constexpr uint32_t kRoundB = 64u * U;  // bytes of a span one round covers
@@ -529,10 +539,10 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
     B d{};
     if constexpr (!kStrided) {
       const uint32_t qc = min(p0 + lane, n - 1);
-      const uint64_t o = off[qc];
+      const uint64_t o = (uint64_t)off[qc];
       d.olo = (uint32_t)o;
       d.ohi = (uint32_t)(o >> 32);
-      d.l = len[qc];
+      d.l = (uint32_t)len[qc];
       d.sd = kSeed ? seed[qc] : 0u;
       d.lp = kParity ? parity[qc] : 0u;
     } else {
@@ -743,7 +753,8 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
 
 }  // namespace
 
-int launch_spans_quad(const void* base, const uint64_t* off, const uint32_t* len,
+template <typename OffT, typename LenT>
+int launch_spans_quad(const void* base, const OffT* off, const LenT* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int u, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream) {
@@ -755,13 +766,16 @@ int launch_spans_quad(const void* base, const uint64_t* off, const uint32_t* len
   const dim3 grid((uint32_t)blocks), blk(kBlock);
   const uint8_t* b = static_cast<const uint8_t*>(base);
   const uint32_t remap = (uint32_t)tuning().xcd_remap;
+  constexpr bool kWide = sizeof(OffT) == 8;
 #define UINET_QUAD(U, P, SD, ST)                                                             \
-  hipLaunchKernelGGL((k_spans_quad<U, P, SD, ST>), grid, blk, 0, stream, b, off, len, seed, \
-                     parity, out, n, flags, remap, stride, slen)
+  hipLaunchKernelGGL((k_spans_quad<U, P, SD, ST, OffT, LenT>), grid, blk, 0, stream, b, off, \
+                     len, seed, parity, out, n, flags, remap, stride, slen)
 #define UINET_QUAD_U(U)                                          \
-  if (strided) {                                                 \
-    if (seed) UINET_QUAD(U, false, true, true);                  \
-    else UINET_QUAD(U, false, false, true);                      \
+  if (strided) { /* wide descriptors only: none are read */     \
+    if constexpr (kWide) {                                       \
+      if (seed) UINET_QUAD(U, false, true, true);                \
+      else UINET_QUAD(U, false, false, true);                    \
+    }                                                            \
   } else if (parity) {                                           \
     if (seed) UINET_QUAD(U, true, true, false);                  \
     else UINET_QUAD(U, true, false, false);                      \
@@ -779,7 +793,8 @@ int launch_spans_quad(const void* base, const uint64_t* off, const uint32_t* len
   return check_launch();
 }
 
-int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len,
+template <typename OffT, typename LenT>
+int launch_spans_lean(const void* base, const OffT* off, const LenT* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream) {
@@ -801,13 +816,16 @@ int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len
   const dim3 grid((uint32_t)blocks), blk(kBlock);
   const uint8_t* b = static_cast<const uint8_t*>(base);
   const uint32_t remap = (uint32_t)tuning().xcd_remap;
+  constexpr bool kWide = sizeof(OffT) == 8;
 #define UINET_LEAN(G, P, SD, ST)                                                              \
-  hipLaunchKernelGGL((k_spans_lean<G, P, SD, ST>), grid, blk, 0, stream, b, off, len, seed, \
-                     parity, out, n, flags, remap, stride, slen)
+  hipLaunchKernelGGL((k_spans_lean<G, P, SD, ST, OffT, LenT>), grid, blk, 0, stream, b, off, \
+                     len, seed, parity, out, n, flags, remap, stride, slen)
 #define UINET_LEAN_G(G)                                          \
-  if (strided) {                                                 \
-    if (seed) UINET_LEAN(G, false, true, true);                  \
-    else UINET_LEAN(G, false, false, true);                      \
+  if (strided) { /* wide descriptors only: none are read */     \
+    if constexpr (kWide) {                                       \
+      if (seed) UINET_LEAN(G, false, true, true);                \
+      else UINET_LEAN(G, false, false, true);                    \
+    }                                                            \
   } else if (parity) {                                           \
     if (seed) UINET_LEAN(G, true, true, false);                  \
     else UINET_LEAN(G, true, false, false);                      \
@@ -824,5 +842,19 @@ int launch_spans_lean(const void* base, const uint64_t* off, const uint32_t* len
 #undef UINET_LEAN
   return check_launch();
 }
+
+// wide (uinet_cksum_spans, strided) and packed (uinet_cksum_spans32) descriptors
+#define UINET_SPANS_INST(OffT, LenT)                                                        \
+  template int launch_spans_quad<OffT, LenT>(const void*, const OffT*, const LenT*,         \
+                                             const uint32_t*, const uint8_t*, uint16_t*,    \
+                                             uint32_t, uint32_t, int, bool, uint64_t,       \
+                                             uint32_t, int, hipStream_t);                   \
+  template int launch_spans_lean<OffT, LenT>(const void*, const OffT*, const LenT*,         \
+                                             const uint32_t*, const uint8_t*, uint16_t*,    \
+                                             uint32_t, uint32_t, int, bool, uint64_t,       \
+                                             uint32_t, int, hipStream_t);
+UINET_SPANS_INST(uint64_t, uint32_t)
+UINET_SPANS_INST(uint32_t, uint16_t)
+#undef UINET_SPANS_INST
 
 }  // namespace uinet

@@ -4,7 +4,9 @@ device-to-device spread hit every variant alike).
 
   python tools/ab.py --config 3 --variants 'chains_pass=2' 'chains_pass=4' 'chains_pass=8'
 
-Each variant is a comma list of key=value pairs for uinet_cksum_set_tuning.
+Each variant is a comma list of key=value pairs for uinet_cksum_set_tuning;
+the pseudo-key desc=1 launches with packed descriptors (uinet_cksum_spans32 /
+uinet_cksum_chains32) instead of wide ones (desc=0, the default).
 Prints one JSON object: per variant the median / min kernel ms and GB/s.
 """
 from __future__ import annotations
@@ -42,7 +44,12 @@ def main():
     w = bench.build_workload(a.config, None, 0)
     out = torch.empty(w["n"], dtype=torch.uint16, device="cuda")
     s = torch.cuda.current_stream()
-    launch = bench.make_launch(a.config, w, a.api, out)
+    if a.config in bench.CHAIN_CONFIGS:
+        w["packed"] = u.pack_segments(w["seg_off"], w["seg_len"])
+    elif a.api == "spans":
+        w["packed"] = u.pack_segments(w["off"], w["len"])
+    launches = {0: bench.make_launch(a.config, w, a.api, out),
+                1: bench.make_launch(a.config, w, a.api, out, "packed") if "packed" in w else None}
     variants = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(",") if kv)
                 for v in a.variants]
     # Every key any variant names goes back to its default before each variant
@@ -50,16 +57,22 @@ def main():
     # had set, so e.g. "spans_pipe=1" after "blocks_per_cu=4096" ran at 4096.)
     for v in variants:
         for k in v:
+            if k == "desc":
+                if launches.get(v[k]) is None:
+                    raise SystemExit(f"tools/ab.py: desc={v[k]} does not apply here")
+                continue
             if k not in DEFAULTS:
                 raise SystemExit(f"tools/ab.py: no default recorded for knob {k!r}")
     times = {i: [] for i in range(len(variants))}
     ref = None
     for r in range(a.rounds):
         for i, v in enumerate(variants):
-            for k in {k for vv in variants for k in vv}:
+            for k in {k for vv in variants for k in vv} - {"desc"}:
                 u.set_tuning(k, DEFAULTS[k])
             for k, val in v.items():
-                u.set_tuning(k, val)
+                if k != "desc":
+                    u.set_tuning(k, val)
+            launch = launches[v.get("desc", 0)]
             launch(s)  # warm
             torch.cuda.synchronize()
             if ref is None:
