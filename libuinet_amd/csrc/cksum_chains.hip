@@ -47,6 +47,8 @@ namespace uinet {
 namespace {
 
 constexpr int kWaves = kBlock / 64;
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short us16x2 __attribute__((ext_vector_type(2)));
 #ifndef UINET_CHAINS_LONGU  // build-time A/B knob (profiles/r01/ab/chains_occ/longu)
 #define UINET_CHAINS_LONGU 4
 #endif
@@ -115,16 +117,25 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
   __shared__ MaskLut lut;
   __shared__ unsigned long long lds_acc[kWaves][2 * kTile];  // (slot, rot) bins
   __shared__ uint32_t lds_pkmark[kWaves][64];  // packet-start markers (slot + 1)
-  __shared__ uint8_t lds_mark[kWaves][kWin];  // segment-start markers (lane + 1) per batch
+  // segment-start markers per batch, (lane + 1) << 8 | meta, and one spare slot
+  // per lane that lanes without a start in the batch write (no exec mask)
+  __shared__ uint16_t lds_mark[kWaves][kWin + 64];
   lut.init();
   for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
-  for (int i = threadIdx.x; i < kWaves * kWin; i += blockDim.x) (&lds_mark[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kWaves * (kWin + 64); i += blockDim.x) (&lds_mark[0][0])[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   unsigned long long* acc = lds_acc[wid];
   uint32_t* pkmark = lds_pkmark[wid];
-  uint8_t* mark = lds_mark[wid];
+  uint16_t* mark = lds_mark[wid];
+  // 16 x (chunk - batch start) of this lane's chunk in pass q, in both halves
+  s16x2 lane16[kPass];
+#pragma unroll
+  for (int q = 0; q < kPass; ++q) {
+    const short x = (short)(16 * (q * 64 + lane));
+    lane16[q] = s16x2{x, x};
+  }
   const uint32_t tiles = (n + kTile - 1) / kTile;
   const uint32_t wstride = gridDim.x * kWaves;
 
@@ -160,7 +171,7 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
     for (int q = 0; q < kPass; ++q) {
       if (lane == 63 || nx[q] != sl[q]) {
         atomicAdd(&acc[sl[q]], (unsigned long long)P[q]);
-        if (lane != 63) atomicAdd(&acc[nx[q]], (unsigned long long)(-(long long)P[q]));
+        if (lane != 63) __atomic_fetch_sub(&acc[nx[q]], (unsigned long long)P[q], __ATOMIC_RELAXED);
       }
     }
   };
@@ -266,18 +277,32 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint64_t R0 = readlane_u64(c0_lo, c0_hi, lf);
       const uint64_t rel = c0 - R0 + (1ull << 31);  // R0 - 2 GiB .. R0 + 2 GiB
       const bool window = __ballot(nch_l != 0 && rel >= (1ull << 32) - (1ull << 16)) == 0;
-      const uint32_t q0 = head + 16u * cst;  // < 2^20
-      const uint32_t recA = q0 | (meta << 20);
-      const uint32_t recB = q0 + eff;
+      // The segment's kept bytes [q0, q0 + eff) in list bytes (q0 < 2^20),
+      // as a pair of 16-bit halves: a chunk's mask bounds are this pair minus
+      // 16 x its list chunk, exact in 16 bits for the chunk's own segment
+      // (|q0 - 16 c| < 16 kListMax + 2 KiB) and computed modulo 2^16 per half.
+      const uint32_t q0 = head + 16u * cst;
+      const uint32_t r16 = (q0 & 0xffffu) | ((q0 + eff) << 16);
+      const uint16_t mval = (uint16_t)(((uint32_t)lane + 1u) << 8 | meta);
       const uint64_t dk = c0 - 16ull * cst;
       const uint32_t dkr = (uint32_t)rel - 16u * cst;  // mod 2^32; + 16 c lands in range
       const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(base + (R0 - (1ull << 31)));
       uint32_t carry_seg1 = 0;  // segment + 1 of the chunk before the batch
       // Issue the batch at list chunk b into (v, key): segment lookup, mask
       // index and bin, loads.  Nothing here waits for packet bytes.
+      //   * lookup: the batch's segment starts are marked in LDS with
+      //     (lane + 1) << 8 | meta; a max-scan gives every chunk its segment
+      //     and its bin (meta = slot << 1 | rot) in one value, carried across
+      //     passes as a scalar max;
+      //   * key: the segment's 16-bit pair (kept bytes relative to the batch)
+      //     minus the chunk's 16 x position, clamped to [0, 16] by two packed
+      //     16-bit ops, becomes the mask-table index lo * 17 + hi and the bin
+      //     in one v_dot2 (a chunk past the list end clamps to the empty mask);
+      //   * two ds_bpermutes per chunk: the pair and the window offset.
       auto issue = [&](uint32_t b, u32x4 (&v)[kPass], uint32_t (&key)[kPass], auto kWindow) {
         const bool mk = nch_l != 0 && cst >= b && cst < b + kWin;
-        if (mk) mark[cst - b] = (uint8_t)(lane + 1);
+        const uint32_t mslot = mk ? cst - b : (uint32_t)(kWin + lane);
+        mark[mslot] = mval;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         uint32_t sc1[kPass];
 #pragma unroll
@@ -290,31 +315,37 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
           sc1[q] = max(sc1[q], carry_seg1);
           carry_seg1 = max(carry_seg1, last);
         }
+        const short b16 = (short)(16u * b);
+        const s16x2 rb = __builtin_bit_cast(s16x2, r16) - s16x2{b16, b16};
+        const uint32_t rbw = __builtin_bit_cast(uint32_t, rb);
 #pragma unroll
         for (int q = 0; q < kPass; ++q) {
           const uint32_t c = b + (uint32_t)(q * 64 + lane);
-          const bool in = c < C;
-          const uint32_t cc = in ? c : C - 1;  // past the end: the last chunk, masked
-          const int seg = (int)sc1[q] - 1;
-          // cross-lane reads stay outside any condition (a ds_bpermute under
-          // a partial exec mask reads 0 from the inactive source lanes)
-          const uint32_t a = (uint32_t)__shfl(recA, seg);
-          const uint32_t bq = (uint32_t)__shfl(recB, seg);
-          const int base16 = 16 * (int)c;
-          const int s_lo = (int)(a & 0xfffffu) - base16;
-          const int s_hi = in ? (int)bq - base16 : s_lo;
-          key[q] = MaskLut::index(s_lo, s_hi) | ((a >> 20) << 16);
+          const uint32_t cc = min(c, C - 1);  // past the end: the last chunk, masked
+          // byte address of the segment's lane for ds_bpermute; cross-lane
+          // reads stay outside any condition (a ds_bpermute under a partial
+          // exec mask reads 0 from the inactive source lanes)
+          const int src = (int)(sc1[q] >> 6) - 4;  // meta < 64 shifts out
+          const s16x2 pr =
+              __builtin_bit_cast(s16x2, (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)rbw)) -
+              lane16[q];
+          const s16x2 cl = __builtin_elementwise_min(__builtin_elementwise_max(pr, s16x2{0, 0}),
+                                                     s16x2{16, 16});
+          // meta (byte 0 of the mark) into byte 2: one v_perm
+          key[q] = __builtin_amdgcn_udot2(__builtin_bit_cast(us16x2, cl), us16x2{17, 1},
+                                          __builtin_amdgcn_perm(0u, sc1[q], 0x0c000c0cu), false);
           if constexpr (decltype(kWindow)::value) {
-            const uint32_t d = (uint32_t)__shfl(dkr, seg);
+            const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)dkr);
             v[q] = load_chunk_buf(rsrc, d + 16u * cc);
           } else {
-            const uint32_t lo32 = (uint32_t)__shfl((uint32_t)dk, seg);
-            const uint32_t hi32 = (uint32_t)__shfl((uint32_t)(dk >> 32), seg);
+            const uint32_t lo32 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)dk);
+            const uint32_t hi32 =
+                (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(dk >> 32));
             v[q] = load_chunk(base + ((((uint64_t)hi32 << 32) | lo32) + 16ull * cc));
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (mk) mark[cst - b] = 0;
+        mark[mslot] = 0;
       };
       auto run = [&](auto kWindow) {
         for (uint32_t b = 0; b < C; b += kWin) {

@@ -1266,11 +1266,10 @@ int main(int argc, char** argv) {
 #define KARGS                                                                   \
   dim3(kBlock), 0, 0, d.arena, d.seg_off, d.seg_len, d.pkt_seg, d.len, d.skip, nullptr, o, d.n, \
       0u, 128u
-  // lab14: the library's kernel with the marker / the bitmap segment lookup,
-  // launched directly (build with -DUINET_CHAINS_LAB_NOLOAD for the no-load
-  // ablation of both)
-  ADD("direct marker lookup", true, hipLaunchKernelGGL((k_chains_pipe<2, 32, false, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
-  ADD("direct bitmap lookup", true, hipLaunchKernelGGL((k_chains_pipe<2, 32, true, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
+  // lab14: the library's kernel launched directly (build with
+  // -DUINET_CHAINS_LAB_NOLOAD for the no-load ablation); the bitmap lookup it
+  // was compared with was removed in round 3 (profiles/r03/pruned/)
+  ADD("direct", true, hipLaunchKernelGGL((k_chains_pipe<2, 32, uint64_t, uint32_t>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   // lab1: one lane per segment
   ADD("lps<2,32>", true, hipLaunchKernelGGL((lab::k_lps<2, 32>), dim3(grid_for_tiles(d.n, 32)), KARGS))
   ADD("lps<4,32>", true, hipLaunchKernelGGL((lab::k_lps<4, 32>), dim3(grid_for_tiles(d.n, 32)), KARGS))
