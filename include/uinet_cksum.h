@@ -310,14 +310,20 @@ int uinet_cksum_unregister_host(void *base);
  *   (0xffff for a good packet, as if_loop.c:96-101 sets it).
  * UDP covers uh_ulen bytes (udp_usrreq.c:404-412); fragments, truncated
  * chains and non-IP frames get no L4 marks.
- * IPv6 (UINET_RX_IPV6): TCP or UDP directly after the fixed header gets the
- * same CSUM_DATA_VALID_IPV6 | CSUM_PSEUDO_HDR marks over the IPv6 pseudo
- * header (in6_cksum.c:86-126), read back by tcp_input.c:627-639 and
- * udp6_usrreq.c:233-246.  No marks for: extension headers (fragments set
- * UINET_RX_FRAG), jumbograms (ip6_plen 0), truncated chains, UDP whose
- * uh_ulen differs from ip6_plen (udps_badlen) or whose uh_sum is 0
- * (UINET_RX_NOSUM; an error in IPv6), and link-local / interface-local
- * addresses carrying a zone word, which ip6_input.c:658-661 drops. */
+ * IPv6 (UINET_RX_IPV6): TCP or UDP after the fixed header and any
+ * hop-by-hop (first only), destination-options and routing headers the stack
+ * walks past (ip6_input.c:906-913,986-1019, dest6.c:62-123, route6.c:59-108)
+ * gets the same CSUM_DATA_VALID_IPV6 | CSUM_PSEUDO_HDR marks over the IPv6
+ * pseudo header (in6_cksum.c:86-126) and the transport's 40 + ip6_plen - off0
+ * bytes, read back by tcp_input.c:627-639 and udp6_usrreq.c:216-246.  No
+ * marks for: fragment headers anywhere in the chain (UINET_RX_FRAG; frag6
+ * reassembles first), routing headers with segments left (dropped), more
+ * than 15 headers, jumbograms (ip6_plen 0), truncated chains, UDP whose
+ * uh_ulen differs from the transport length (udps_badlen) or whose uh_sum is
+ * 0 (UINET_RX_NOSUM; an error in IPv6), and link-local / interface-local
+ * addresses carrying a zone word, which ip6_input.c:658-661 drops.
+ * TX (CSUM_TCP_IPV6 / CSUM_UDP_IPV6) finds the transport past the same
+ * extension headers, as an offloading NIC must. */
 int uinet_cksum_rx_offload(struct mbuf *const *m, int n, int l2len,
     uint8_t *status);
 

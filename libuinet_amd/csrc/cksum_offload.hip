@@ -120,8 +120,7 @@ uint32_t fold16(uint64_t s) {
   return (uint32_t)s;
 }
 
-// The fixed IPv6 header and the first 8 bytes after it.  Extension headers
-// are not walked: a packet whose ip6_nxt is not TCP or UDP gets no L4 job.
+// The fixed IPv6 header and the first 8 bytes after it.
 struct Ip6 {
   int l3 = 0;
   int plen = 0;  // ip6_plen
@@ -154,12 +153,40 @@ bool ip6_zone_embedded(const uint8_t* a) {
   return (ll || mc) && (a[2] | a[3]) != 0;
 }
 
+// The extension headers between the fixed IPv6 header and the transport, as
+// the stack walks them: hop-by-hop only first (ip6_input.c:906-913), then the
+// next-header loop (:986-1019) through destination options (dest6.c:62-123)
+// and routing headers (route6.c:59-108: segments left 0 is skipped, anything
+// else dropped on receive); at most 15 headers (ip6_hdrnestlimit).  A
+// fragment header (frag6.c:165) stops the walk: the stack reassembles first.
+// Returns 1 with *off (the transport header's offset from the IPv6 header)
+// and *nxt at the first other header, 0 at a fragment header, -1 when the
+// stack would drop the packet or the walk leaves the payload (ip6_plen).
+int ip6_walk(const MbufHdr* m, const Ip6& ip, bool rx, int* off, int* nxt) {
+  int o = 40, x = ip.nxt;
+  for (int k = 0; k < 15; k++) {
+    if (x == 0 && k != 0) return -1;  // hop-by-hop after the first header
+    if (x != 0 && x != 43 && x != 60) {
+      if (o > 40 + ip.plen) return -1;
+      *off = o;
+      *nxt = x;
+      return x == 44 ? 0 : 1;
+    }
+    uint8_t e[4];
+    if (o + 8 > 40 + ip.plen || chain_read(m, ip.l3 + o, e, 4) < 4) return -1;
+    if (rx && x == 43 && e[3] != 0) return -1;  // segments left: route6.c:99-105
+    x = e[0];
+    o += (e[1] + 1) * 8;
+  }
+  return -1;
+}
+
 // in6_cksum.c:86-126 for wire addresses (no embedded zone): htonl(len),
-// three zero bytes and nxt, then both addresses, as little-endian 16-bit
-// words; folded so it fits a job seed.
-uint32_t pseudo6_seed(const Ip6& ip, uint32_t len) {
+// three zero bytes and the transport's nxt, then both addresses, as
+// little-endian 16-bit words; folded so it fits a job seed.
+uint32_t pseudo6_seed(const Ip6& ip, uint32_t len, int nxt) {
   uint64_t s = (uint64_t)bswap16((uint16_t)(len >> 16)) + bswap16((uint16_t)len) +
-               bswap16((uint16_t)ip.nxt);
+               bswap16((uint16_t)nxt);
   for (int i = 0; i < 32; i += 2) s += (uint64_t)(ip.addr[i] | ip.addr[i + 1] << 8);
   return fold16(s);
 }
@@ -186,25 +213,37 @@ struct TxPlan {
   uint8_t st = 0;
 };
 
-// RX IPv6: tcp_input.c:627-639 (tlen = ip6_plen for a bare header) and
-// udp6_usrreq.c:216-246 (uh_ulen must equal the payload length, uh_sum 0 is
-// an error).  Returns the L4 job, or m == nullptr for none.
+// RX IPv6: tcp_input.c:627-639 (tlen = 40 + ip6_plen - off0, the transport
+// after the extension headers) and udp6_usrreq.c:216-246 (uh_ulen must equal
+// that length, uh_sum 0 is an error).  Returns the L4 job, or m == nullptr
+// for none.
 Job rx6_job(const MbufHdr* m, const Ip6& ip, uint8_t* st) {
   const Job none{nullptr, 0, 0, 0u};
-  if (ip.nxt == 44) *st |= UINET_RX_FRAG;
-  if (ip.plen == 0 || chain_len(m) < (long)ip.l3 + 40 + ip.plen) return none;  // jumbo, short
+  int off = 40, nxt = ip.nxt;
+  const int w = ip.plen ? ip6_walk(m, ip, true, &off, &nxt) : -1;
+  if (w == 0 || ip.nxt == 44) *st |= UINET_RX_FRAG;
+  if (w != 1) return none;
+  if (chain_len(m) < (long)ip.l3 + 40 + ip.plen) return none;  // ip6s_tooshort
   if (ip6_zone_embedded(ip.addr) || ip6_zone_embedded(ip.addr + 16)) return none;
-  if (ip.nxt == 17) {
-    if (ip.l4_have < 8) return none;
-    if (be16(ip.l4 + 4) != ip.plen) return none;  // udps_badlen
-    if (be16(ip.l4 + 6) == 0) {                    // udps_nosum
+  const int tlen = 40 + ip.plen - off;
+  if (nxt == 17) {
+    uint8_t u[8];
+    const uint8_t* uh = ip.l4;
+    if (off != 40) {
+      if (chain_read(m, ip.l3 + off, u, 8) < 8) return none;
+      uh = u;
+    } else if (ip.l4_have < 8) {
+      return none;
+    }
+    if (be16(uh + 4) != tlen) return none;  // udps_badlen
+    if (be16(uh + 6) == 0) {                // udps_nosum
       *st |= UINET_RX_NOSUM;
       return none;
     }
-  } else if (ip.nxt != 6) {
+  } else if (nxt != 6) {
     return none;
   }
-  return Job{m, ip.l3 + 40 + ip.plen, ip.l3 + 40, pseudo6_seed(ip, (uint32_t)ip.plen)};
+  return Job{m, ip.l3 + 40 + ip.plen, ip.l3 + off, pseudo6_seed(ip, (uint32_t)tlen, nxt)};
 }
 
 thread_local std::vector<Job> t_jobs;
@@ -331,17 +370,23 @@ int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
       int l3 = 0;
       const int ver = (fl & kCsumTso) ? 0 : l3_locate(m, l2len, &l3);
       if (ver == 6) {  // in6_delayed_cksum, ip6_output.c:188-209,978-981
+        // As an offloading NIC must (ip6_output.c:966-981 leaves CSUM_*_IPV6
+        // to a driver that advertises it, extension headers or not), the
+        // transport is found past the extension headers; the seed already
+        // in its checksum field holds the final destination.
         Ip6 ip6;
-        if (!(fl & (kCsumTcpIpv6 | kCsumUdpIpv6)) || !parse_ip6(m, l3, &ip6) || ip6.plen == 0) {
+        int off = 40, nxt = 0;
+        if (!(fl & (kCsumTcpIpv6 | kCsumUdpIpv6)) || !parse_ip6(m, l3, &ip6) || ip6.plen == 0 ||
+            ip6_walk(m, ip6, false, &off, &nxt) != 1) {
           p.st = UINET_TX_SKIP;
           continue;
         }
         p.st = UINET_TX_IPV6;
         p.udp = (fl & kCsumUdpIpv6) != 0;
         p.clear = kCsumTcpIpv6 | kCsumUdpIpv6;
-        p.l4_store = l3 + 40 + pkthdr_of(m)->csum_data;
+        p.l4_store = l3 + off + pkthdr_of(m)->csum_data;
         p.l4_job = true;
-        jobs[2 * (size_t)i + 1] = {m, l3 + 40 + ip6.plen, l3 + 40, 0u};
+        jobs[2 * (size_t)i + 1] = {m, l3 + 40 + ip6.plen, l3 + off, 0u};
         continue;
       }
       Ip4 ip;

@@ -16,12 +16,18 @@ checksum, IP options, 802.1Q tags, fragments, other protocols, non-IP
 frames, and (RX) corrupted headers / payloads / checksum fields.
 
 With ``ipv6 > 0`` that share of the IP frames is IPv6 instead (Ethernet type
-0x86dd): TCP / UDP directly after the fixed header with the in6_cksum_pseudo
-seed in the checksum field and CSUM_TCP_IPV6 / CSUM_UDP_IPV6 (tcp_output.c:
+0x86dd): TCP / UDP after the fixed header with the in6_cksum_pseudo seed in
+the checksum field and CSUM_TCP_IPV6 / CSUM_UDP_IPV6 (tcp_output.c:
 1069-1071, udp6_usrreq.c:786), UDP with a zero checksum, fragments (next
-header 44), hop-by-hop options in front of TCP, ICMPv6, and global,
-link-local and (rarely) zone-carrying link-local addresses.  The IPv4 frames'
-random stream does not depend on ``ipv6``.
+header 44), ICMPv6, and global, link-local and (rarely) zone-carrying
+link-local addresses.  12 % of the IPv6 TCP / UDP frames carry extension
+headers (``ext6``): hop-by-hop and destination options (PadN), routing
+headers with no segments left, a routing header with one segment left
+(``rt_left``: the receiver drops it, route6.c:99-105; the seed holds the
+final destination, the address in the routing header) or a fragment header
+after hop-by-hop options (``frag_ext``, no offload flags).  ``nxt6`` is the
+transport protocol.  The IPv4 frames' random stream does not depend on
+``ipv6``.
 """
 from __future__ import annotations
 
@@ -83,7 +89,10 @@ class FrameBatch:
                            [0.62, 0.24, 0.04, 0.05, 0.05, 0.0])
         self.kinds = kinds
         self.v6 = (rng6.random(n) < ipv6) & (kinds != "arp")
-        self.ext6 = self.v6 & (kinds == "tcp") & (rng6.random(n) < 0.06)
+        self.ext6 = self.v6 & np.isin(kinds, ["tcp", "udp"]) & (rng6.random(n) < 0.12)
+        self.rt_left = np.zeros(n, bool)
+        self.frag_ext = np.zeros(n, bool)
+        self.nxt6 = np.zeros(n, np.int64)
         self.addr6 = np.zeros((n, 32), np.uint8)
         hdr_slot = 256
         pay = np.where(rng.random(n) < 0.15, rng.integers(0, 64, n), rng.integers(64, 1461, n))
@@ -132,12 +141,54 @@ class FrameBatch:
         self.tx = MbufChains(self.arena, seg_off, seg_len, pkt_seg)
         self.set_tx_flags()
 
+    def _ext_chain(self, i, k, rng):
+        """The extension headers of frame i as (next-header type, bytes) in
+        wire order (each header's first byte is filled in by the caller), and
+        the final destination a routing header with segments left carries."""
+        if k == "frag":
+            return [(44, rng.integers(0, 256, 8, dtype=np.uint8))], None
+        if not self.ext6[i]:
+            return [], None
+
+        def opts(n8):  # n8 x 8 bytes of options: one PadN
+            h = np.zeros(8 * n8, np.uint8)
+            h[1], h[2], h[3] = n8 - 1, 1, 8 * n8 - 4
+            return h
+
+        def rt(left, final):
+            h = np.zeros(24, np.uint8)
+            h[1], h[2], h[3] = 2, 2, left  # type 2 (one address), segments left
+            h[8:24] = final
+            return h
+
+        final = None
+        r = rng.random()
+        if r < 0.30:
+            chain = [(0, opts(1))]
+        elif r < 0.50:
+            chain = [(60, opts(2))]
+        elif r < 0.65:
+            chain = [(0, opts(1)), (43, rt(0, _addr6(rng)))]
+        elif r < 0.80:
+            chain = [(0, opts(1)), (60, opts(1)), (43, rt(0, _addr6(rng)))]
+        elif r < 0.88:
+            chain = [(60, opts(1)), (43, rt(0, _addr6(rng))), (60, opts(1))]
+        elif r < 0.94:
+            final = _addr6(rng)
+            chain = [(43, rt(1, final))]
+            self.rt_left[i] = True
+        else:
+            chain = [(0, opts(1)), (44, rng.integers(0, 256, 8, dtype=np.uint8))]
+            self.frag_ext[i] = True
+        return chain, final
+
     def _header6(self, i, k, p, l2, vlan, rng):
-        """Link + IPv6 (+ one extension header) + L4 header of frame i."""
+        """Link + IPv6 (+ extension headers) + L4 header of frame i."""
         tag = l2 and rng.random() < vlan
         l3 = (18 if tag else 14) if l2 else 0
-        ext = 8 if (k == "frag" or self.ext6[i]) else 0
         nxt = {"tcp": 6, "frag": 6, "udp": 17, "udp0": 17, "icmp": 58}[k]
+        chain, final = self._ext_chain(i, k, rng)
+        ext = sum(int(b.size) for _, b in chain)
         l4h = 20 if nxt == 6 else 8
         plen = ext + l4h + p
         h = np.zeros(l3 + 40 + ext + l4h, np.uint8)
@@ -152,23 +203,26 @@ class FrameBatch:
         ip6[1:4] = rng.integers(0, 256, 3, dtype=np.uint8)
         ip6[1] &= 0x0F
         ip6[4:6] = (plen >> 8, plen & 0xFF)
-        ip6[6] = 44 if k == "frag" else 0 if ext else nxt
+        ip6[6] = chain[0][0] if chain else nxt
         ip6[7] = 64
         src, dst = _addr6(rng), _addr6(rng)
         ip6[8:24], ip6[24:40] = src, dst
         self.addr6[i] = np.concatenate([src, dst])
-        if ext:  # fragment header, or hop-by-hop with one PadN option
-            e = h[l3 + 40:l3 + 48]
-            e[0] = nxt
-            e[2:8] = rng.integers(0, 256, 6, dtype=np.uint8) if k == "frag" else (1, 4, 0, 0, 0, 0)
+        o = l3 + 40
+        for j, (_, b) in enumerate(chain):
+            h[o:o + b.size] = b
+            h[o] = chain[j + 1][0] if j + 1 < len(chain) else nxt
+            o += b.size
         l4 = h[l3 + 40 + ext:]
         l4[:] = rng.integers(0, 256, l4h, dtype=np.uint8)
+        fdst = dst if final is None else final  # the pseudo header's destination
+        offload = k != "frag" and not self.frag_ext[i]
         fl, cd = 0, 0
         if nxt == 6:
             l4[12] = 0x50
-            seed16 = pseudo6(src, dst, l4h + p, 6)
+            seed16 = pseudo6(src, fdst, l4h + p, 6)
             l4[16:18] = (seed16 & 0xFF, seed16 >> 8)
-            if not ext:
+            if offload:
                 fl, cd = CSUM_TCP_IPV6, 16
         elif nxt == 17:
             ulen = 8 + p
@@ -176,11 +230,12 @@ class FrameBatch:
             if k == "udp0":
                 l4[6:8] = 0
             else:
-                seed16 = pseudo6(src, dst, ulen, 17)
+                seed16 = pseudo6(src, fdst, ulen, 17)
                 l4[6:8] = (seed16 & 0xFF, seed16 >> 8)
-                fl, cd = CSUM_UDP_IPV6, 6
+                if offload:
+                    fl, cd = CSUM_UDP_IPV6, 6
         self.flags[i], self.cdata[i] = fl, cd
-        self.l3[i], self.hlen[i] = l3, 40 + ext
+        self.l3[i], self.hlen[i], self.nxt6[i] = l3, 40 + ext, nxt
         return h
 
     def _header4(self, i, k, p, l2, vlan, rng):

@@ -20,14 +20,23 @@
  *
  * IPv6 frames (Ethernet type 0x86dd, or version 6 at l2len) go the IPv6 way:
  *   RX  sys/netinet6/ip6_input.c          short chains and embedded zones
- *                                         (:658-661) are dropped; the next
- *                                         header picks the transport
- *       sys/netinet/tcp_input.c:627-639   th_sum = in6_cksum(m, TCP, 40, tlen)
- *       sys/netinet6/udp6_usrreq.c:216-246 uh_ulen == payload length, uh_sum
- *                                         != 0, in6_cksum(m, UDP, 40, ulen)
+ *                                         (:658-661) are dropped; hop-by-hop
+ *                                         options first (:906-913), then the
+ *                                         next-header loop (:986-1019):
+ *       sys/netinet6/dest6.c:62-123       destination options skipped
+ *       sys/netinet6/route6.c:59-108      routing header skipped when its
+ *                                         segments left is 0, else dropped
+ *       sys/netinet6/frag6.c:165          reassembly first (no verdict here)
+ *       sys/netinet/tcp_input.c:627-639   th_sum = in6_cksum(m, TCP, off0,
+ *                                         40 + ip6_plen - off0)
+ *       sys/netinet6/udp6_usrreq.c:216-246 uh_ulen == that length, uh_sum
+ *                                         != 0, in6_cksum(m, UDP, off, ulen)
  *     with the same CSUM_DATA_VALID(_IPV6) | CSUM_PSEUDO_HDR marks;
  *   TX  sys/netinet6/ip6_output.c:188-209,966-981  in6_delayed_cksum(m,
- *                                         ip6_plen, sizeof(struct ip6_hdr))
+ *                                         transport length, transport offset)
+ *                                         -- the transport found past the
+ *                                         extension headers, as a NIC that
+ *                                         advertises CSUM_*_IPV6 must
  *
  * Chains whose link header reaches past the first mbuf are viewed through
  * a private copy of their mbuf headers (what m_adj would leave).
@@ -174,28 +183,71 @@ zone_embedded(const uint8_t *a)
 	return (ll || mc) && (a[2] || a[3]);
 }
 
+/*
+ * The header chain after the fixed IPv6 header of `ipm` (m_data at the IPv6
+ * header, payload length plen): hop-by-hop (0) only as the first header,
+ * destination options (60) and routing (43) headers are (len + 1) * 8 bytes,
+ * a routing header with segments left is dropped on receive, at most 15
+ * headers.  Returns 1 and the transport's offset / protocol, 0 at a fragment
+ * header (44), -1 for a dropped packet.
+ */
+static int
+walk6(const struct oracle_mbuf *ipm, int plen, int first, int rx, int *off, int *nxt)
+{
+	int o = 40, x = first, k;
+	uint8_t e[4];
+
+	for (k = 0; k < 15; k++) {
+		if (x == 0 && k > 0)
+			return -1;
+		if (x == 44) {
+			*off = o;
+			*nxt = x;
+			return o <= 40 + plen ? 0 : -1;
+		}
+		if (x != 0 && x != 60 && x != 43) {
+			if (o > 40 + plen)
+				return -1;
+			*off = o;
+			*nxt = x;
+			return 1;
+		}
+		if (o + 8 > 40 + plen || chain_bytes(ipm, o, e, 4) < 4)
+			return -1;
+		if (rx && x == 43 && e[3] != 0)
+			return -1;	/* route6.c:99-105 */
+		x = e[0];
+		o += 8 * (e[1] + 1);
+	}
+	return -1;
+}
+
 /* One received IPv6 frame, m_data at the IPv6 header in `ipm`. */
 static uint8_t
 rx6(struct oracle_mbuf *m, struct oracle_mbuf *ipm, const uint8_t *h, int got, long avail)
 {
-	uint8_t st = S_RX_IPV6;
-	int plen = h[4] << 8 | h[5], nxt = h[6], sum;
+	uint8_t st = S_RX_IPV6, u[8];
+	int plen = h[4] << 8 | h[5], nxt = h[6], off = 40, w = -1, tlen, sum;
 
-	if (nxt == 44)
+	(void)got;
+	if (plen)
+		w = walk6(ipm, plen, h[6], 1, &off, &nxt);
+	if (w == 0 || h[6] == 44)
 		st |= S_RX_FRAG;	/* frag6_input reassembles first */
-	if (plen == 0 || avail < 40 + (long)plen)
-		return st;		/* jumbogram (hop-by-hop), ip6s_tooshort */
+	if (w != 1 || avail < 40 + (long)plen)
+		return st;		/* dropped, jumbogram (hop-by-hop), ip6s_tooshort */
 	if (zone_embedded(h + 8) || zone_embedded(h + 24))
 		return st;		/* ip6s_badscope */
+	tlen = 40 + plen - off;
 	if (nxt == 17) {
-		if (got < 48 || (h[44] << 8 | h[45]) != plen)
+		if (chain_bytes(ipm, off, u, 8) < 8 || (u[4] << 8 | u[5]) != tlen)
 			return st;	/* udps_badlen */
-		if ((h[46] | h[47]) == 0)
+		if ((u[6] | u[7]) == 0)
 			return st | S_RX_NOSUM;
 	} else if (nxt != 6) {
 		return st;
 	}
-	sum = oracle_in6_cksum(ipm, (uint8_t)nxt, 40, (uint32_t)plen);
+	sum = oracle_in6_cksum(ipm, (uint8_t)nxt, (uint32_t)off, (uint32_t)tlen);
 	st |= S_RX_L4 | (sum == 0 ? S_RX_L4_OK : 0);
 	if (m->m_flags & O_M_PKTHDR) {
 		*csum_flags(m) |= O_CSUM_DATA_VALID | O_CSUM_PSEUDO_HDR;
@@ -297,9 +349,9 @@ oracle_tx_offload(struct oracle_mbuf *const *mv, int n, int l2len, uint8_t *stat
 		}
 		fl = *csum_flags(m);
 		if (!(fl & O_CSUM_TSO) && (l3 = ip_offset(m, l2len, &ver)) >= 0 && ver == 6) {
-			/* in6_delayed_cksum(m, plen, sizeof(struct ip6_hdr)) */
+			/* in6_delayed_cksum(m, transport length, transport offset) */
 			uint16_t csum;
-			int plen, offset;
+			int plen, offset, l4 = 40, nxt;
 
 			if (!(fl & (O_CSUM_TCP_IPV6 | O_CSUM_UDP_IPV6)) ||
 			    chain_bytes(m, l3, h, 40) < 40 || (h[0] >> 4) != 6 ||
@@ -308,10 +360,14 @@ oracle_tx_offload(struct oracle_mbuf *const *mv, int n, int l2len, uint8_t *stat
 				goto done;
 			}
 			ipm = adj_view(m, l3, &tmp);
-			csum = oracle_cksum_skip(ipm, 40 + plen, 40);
+			if (walk6(ipm, plen, h[6], 0, &l4, &nxt) != 1) {
+				st = S_TX_SKIP;
+				goto done;
+			}
+			csum = oracle_cksum_skip(ipm, 40 + plen, l4);
 			if ((fl & O_CSUM_UDP_IPV6) && csum == 0)
 				csum = 0xffff;
-			offset = 40 + *csum_data(m);
+			offset = l4 + *csum_data(m);
 			st = S_TX_IPV6;
 			if (offset + 2 > ipm->m_len) {
 				st |= S_TX_L4_LOST;

@@ -139,23 +139,48 @@ def _from_l3(ch, fb, idx):
     return MbufChains.contiguous(arena, 2048 * np.arange(len(bufs)), [len(b) for b in bufs]), bufs
 
 
+def _walk6(b: bytes, rx: bool):
+    """The IPv6 header chain of ``b`` (bytes from the IPv6 header on) as the
+    reference's stack walks it (ip6_input.c:906-913,986-1019, dest6.c:62-123,
+    route6.c:59-108, frag6.c:165): (transport offset, next header), ("frag",
+    offset) at a fragment header, or None for a packet the stack drops."""
+    plen = b[4] << 8 | b[5]
+    o, x = 40, b[6]
+    for k in range(15):
+        if x == 0 and k > 0:
+            return None
+        if x not in (0, 43, 60):
+            if o > 40 + plen:
+                return None
+            return ("frag", o) if x == 44 else (o, x)
+        if o + 8 > 40 + plen or len(b) < o + 4:
+            return None
+        if rx and x == 43 and b[o + 3] != 0:
+            return None
+        x, o = b[o], o + 8 * (b[o + 1] + 1)
+    return None
+
+
 def test_tx6_oracle_against_reference(frames, ora, ref):
-    """IPv6 TX: the frames' checksum-field seeds are the reference's own
-    in6_cksum_pseudo; after the oracle TX hook every handled IPv6 packet
-    verifies to 0 with the reference's in6_cksum, and the handled
-    CSUM_*_IPV6 bits are cleared."""
+    """IPv6 TX, extension headers included: the frames' checksum-field seeds
+    are the reference's own in6_cksum_pseudo; after the oracle TX hook every
+    handled IPv6 packet verifies to 0 with the reference's in6_cksum over
+    its transport (past the extension headers), and the handled CSUM_*_IPV6
+    bits are cleared."""
     fb = frames(seed=13, ipv6=0.5)
     v6 = np.flatnonzero(fb.v6 & ((fb.flags & 0x6000) != 0))
-    assert v6.size > 500
-    for i in v6[:300]:  # the builder's seed == the reference's in6_cksum_pseudo(ip6, len, nxt, 0)
+    assert v6.size > 500 and fb.ext6[v6].sum() > 40
+    for i in v6:  # the builder's seed == the reference's in6_cksum_pseudo(ip6, len, nxt, 0)
+        if fb.rt_left[i] or _zoned(fb.addr6[i][:16]) or _zoned(fb.addr6[i][16:]):
+            continue  # routing header with segments left: the seed holds its final address
         b = np.frombuffer(fb.frame_bytes(i), np.uint8)
-        l3 = int(fb.l3[i])
+        l3, off = int(fb.l3[i]), int(fb.hlen[i])
         ip6 = b[l3:l3 + 40].copy()
-        nxt, plen = int(ip6[6]), int(ip6[4]) << 8 | int(ip6[5])
-        off = l3 + 40 + (16 if nxt == 6 else 6)
-        stored = int(b[off]) | int(b[off + 1]) << 8
-        if not (_zoned(fb.addr6[i][:16]) or _zoned(fb.addr6[i][16:])):
-            assert ref.in6_cksum_pseudo(ip6.ctypes.data, plen, nxt, 0) == stored
+        nxt, plen = int(fb.nxt6[i]), int(ip6[4]) << 8 | int(ip6[5])
+        at = l3 + off + (16 if nxt == 6 else 6)
+        stored = int(b[at]) | int(b[at + 1]) << 8
+        assert _walk6(bytes(b[l3:]), False) == (off, nxt)
+        assert ref.in6_cksum_pseudo(ip6.ctypes.data, plen + 40 - off, nxt, 0) == stored
     st = ora.tx_offload(fb.tx.heads)
     tso = (fb.flags & 0x20) != 0
     want = fb.v6 & ((fb.flags & 0x6000) != 0) & ~tso
@@ -164,12 +189,12 @@ def test_tx6_oracle_against_reference(frames, ora, ref):
     fl, _ = pkthdr_fields(fb.tx)
     assert not (fl[want] & 0x6000).any()
     assert ((st[fb.v6 & ~want] & TX_SKIP) != 0).all()
-    ok = np.array([i for i in np.flatnonzero(want)
+    ok = np.array([i for i in np.flatnonzero(want & ~fb.rt_left)
                    if not (_zoned(fb.addr6[i][:16]) or _zoned(fb.addr6[i][16:]))])
     ch, bufs = _from_l3(fb.tx, fb, ok)
-    nxt = np.array([b[6] for b in bufs])
+    off = fb.hlen[ok]
     plen = np.array([b[4] << 8 | b[5] for b in bufs])
-    assert not ref.in6_cksum_batch(ch.heads, nxt, 40, plen).any()
+    assert not ref.in6_cksum_batch(ch.heads, fb.nxt6[ok], off, plen + 40 - off).any()
 
 
 def test_rx6_oracle_against_reference(frames, ora, ref):
@@ -186,21 +211,25 @@ def test_rx6_oracle_against_reference(frames, ora, ref):
     l4 = np.flatnonzero(fb.v6 & ((st & RX_L4) != 0))
     assert l4.size > 500
     ch, bufs = _from_l3(rx, fb, l4)
-    nxt = np.array([b[6] for b in bufs])
+    walks = [_walk6(b, True) for b in bufs]
+    off = np.array([w[0] for w in walks])
+    nxt = np.array([w[1] for w in walks])
     plen = np.array([b[4] << 8 | b[5] for b in bufs])
     assert set(np.unique(nxt)) <= {6, 17}
-    want = ref.in6_cksum_batch(ch.heads, nxt, 40, plen)
+    want = ref.in6_cksum_batch(ch.heads, nxt, off, plen + 40 - off)
     np.testing.assert_array_equal(cd[l4] ^ 0xFFFF, want)
     np.testing.assert_array_equal((st[l4] & RX_L4_OK) != 0, want == 0)
     assert ((fl[l4] & 0xC00) == 0xC00).all()
     zoned = np.array([_zoned(a[:16]) or _zoned(a[16:]) for a in fb.addr6])
-    clean = fb.v6 & ~bad & ~zoned & ~fb.ext6
-    good = clean & np.isin(fb.kinds, ["tcp", "udp"]) & ((fb.flags & 0x20) == 0)  # TSO: not filled
+    clean = fb.v6 & ~bad & ~zoned
+    dropped = fb.rt_left | fb.frag_ext  # route6 drops; frag6 reassembles first
+    good = clean & ~dropped & np.isin(fb.kinds, ["tcp", "udp"]) & ((fb.flags & 0x20) == 0)
     assert ((st[good] & (RX_L4 | RX_L4_OK)) == (RX_L4 | RX_L4_OK)).all()
+    assert (good & fb.ext6).sum() > 40  # extension headers walked to the transport
     assert not (st[fb.v6 & zoned] & RX_L4).any()
-    assert not (st[fb.v6 & fb.ext6] & RX_L4).any()
+    assert not (st[fb.v6 & dropped] & RX_L4).any()
     assert ((st[clean & (fb.kinds == "udp0")] & RX_NOSUM) != 0).all()
-    assert ((st[clean & (fb.kinds == "frag")] & RX_FRAG) != 0).all()
+    assert ((st[clean & ((fb.kinds == "frag") | fb.frag_ext)] & RX_FRAG) != 0).all()
 
 
 # ---- GPU: engine == oracle ------------------------------------------------------
