@@ -200,7 +200,7 @@ def dispatched_kernel(cfg: str, api: str, w) -> str:
     if g >= 32:
         if pipe == 1 and u == 3:
             return "k_spans_lean"
-        return {0: "k_spans", 1: "k_spans_pp", 2: "k_spans_pp"}[pipe]
+        return "k_spans"
     if g == 4 and pipe == 1 and (api == "spans" or u == 1):
         return "k_spans_quad"
     return "k_spans"

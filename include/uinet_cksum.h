@@ -157,10 +157,7 @@ int uinet_cksum_device_ok(void);
  *                     1 (default) persistent waves with mask-free whole
  *                     chunks and the per-packet work shared across the wave
  *                     (k_spans_lean at 32 / 64 lanes per packet, k_spans_quad
- *                     at 4); 2 = round 2's two-in-flight lane groups at 32 /
- *                     64 lanes (k_spans_pp; ~1-2 % faster warm, slower under
- *                     the platform's power ramp); 0 = one packet per lane
- *                     group, one-shot grid
+ *                     at 4); 0 = one packet per lane group, one-shot grid
  *   "spans_geo"       span kernels: force the lanes-per-packet G and loads
  *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
  *                     16x3, 32x3, 64x2, 64x3); 0 = picked from len_hint

@@ -78,7 +78,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"host_threads", &TuningLive::host_threads, [](int v) { return v >= 1 && v <= 64; }},
       {"spans_geo", &TuningLive::spans_geo, [](int v) { return v == 0 || span_geometry_ok(v); }},
       {"spans_sdesc", &TuningLive::spans_sdesc, [](int v) { return v == 0 || v == 1; }},
-      {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v >= 0 && v <= 2; }},
+      {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v == 0 || v == 1; }},
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
       {"host_group", &TuningLive::host_group, [](int v) { return v >= 1 && v <= 64; }},
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},

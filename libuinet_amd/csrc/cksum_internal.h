@@ -22,7 +22,7 @@ struct Tuning {
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
   int spans_sdesc;     // span kernels: per-wave scalar descriptor loads (0/1)
   int spans_pipe;      // span kernel family: 1 k_spans_lean / k_spans_quad (persistent,
-                       // mask-free whole chunks), 2 k_spans_pp, 0 one-shot k_spans
+                       // mask-free whole chunks), 0 one-shot k_spans
   int spans_geo;       // span kernels: lanes-per-packet G and loads-per-lane U
                        // as G * 16 + U (0 = picked from the mean length)
   int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead, 2 lockstep chase

@@ -162,123 +162,9 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
   }
 }
 
-// k_spans_pp: the scalar-descriptor span kernel with two packets in flight
-// per lane group.  Each group walks its packets p, p + S, p + 2S, ... (S the
-// grid's group count) with two register sets: packet k+1's chunks are loaded
-// before packet k is summed, so a group never waits between packets.  Every
-// load is unconditional (lanes past a span's end, and packets past the
-// group's end, re-load a chunk they already hold or the arena's first chunk,
-// and mask it away), so the compiler's wait for packet k counts packet
-// k+1's loads as still in flight.
-//
-// Why (profiles/r02/cold_ab/): with one packet per group the grid is 512
-// blocks per CU, and in the first launches after an idle gap (the power ramp
-// of a burst) such launches stretch from 0.21 to 0.32 ms for ~100 launches;
-// a pure streaming read does not, nor does a grid of 128 blocks per CU with 4
-// packets per group.  The driver's 5-warmup / 20-step window after a fresh
-// workload build: 0.70-0.85 of HBM peak one-shot, 0.88 with this kernel (3
-// boxes, 4 + 3 runs each).  Warm, back to back, the one-shot grid stays ~5 %
-// faster on config 2 (spans_pipe = 0 keeps it).
-template <int G, int U>
-struct SpanPP {
-  int head, end;  // the span's bytes are [head, end) from its first aligned chunk
-  u32x4 v[U];
-  // Loads the span's first G * U chunks (an empty span re-reads the arena's
-  // first aligned chunk -- base itself may be unaligned, and an unaligned
-  // 16-B read may cross into an unmapped page; lanes past the end re-read
-  // the last chunk) and keeps only what the fold needs.
-  __device__ __forceinline__ void load(const uint8_t* base, uint64_t o, uint32_t len, int gl) {
-    const uint8_t* a = base + o;
-    head = len ? (int)(reinterpret_cast<uintptr_t>(a) & 15) : 0;
-    end = head + (int)len;
-    const uint8_t* c0 = len ? a - head : base - (reinterpret_cast<uintptr_t>(base) & 15);
-    const uint32_t last = len ? ((uint32_t)(end + 15) >> 4) - 1u : 0u;
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = load_chunk(c0 + 16u * min((uint32_t)(u * G + gl), last));
-  }
-  __device__ __forceinline__ uint32_t sum(const MaskLut& lut, int gl) const {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int b = 16 * (u * G + gl);
-      acc += lut.sum_oc(v[u], head - b, end - b);
-    }
-    return acc;
-  }
-};
-
-template <int G, int U, bool kParity, bool kStrided = false>
-__global__ __launch_bounds__(kBlock) void k_spans_pp(const uint8_t* __restrict__ base,
-                                                    const uint64_t* __restrict__ off,
-                                                    const uint32_t* __restrict__ len,
-                                                    const uint32_t* __restrict__ seed,
-                                                    const uint8_t* __restrict__ parity,
-                                                    uint16_t* __restrict__ out, uint32_t n,
-                                                    uint32_t flags, uint32_t remap,
-                                                    uint64_t stride = 0, uint32_t slen = 0) {
-  static_assert(G >= 32, "scalar descriptors: one or two packets per wave");
-  constexpr uint32_t kGroups = kBlock / G;
-  constexpr int kChunks = G * U;
-  __shared__ MaskLut lut;
-  const int gl = threadIdx.x & (G - 1);
-  const uint32_t S = gridDim.x * kGroups;
-  const uint32_t lb = logical_block(remap);
-  uint32_t p = lb * kGroups + threadIdx.x / G;
-  // A packet's descriptors, fetched one packet ahead of its fold: off / len
-  // (and the seed) by scalar loads, the parity byte by a vector load.  No
-  // load sits under a branch, so the wait for a packet's chunks counts every
-  // later load as still in flight.
-  struct Desc {
-    uint64_t o;
-    uint32_t l, sd, lp;
-  };
-  auto desc = [&](uint32_t q) {
-    Desc d;
-    if constexpr (kStrided) {  // the strided API: packet q at q * stride, slen bytes
-      d.o = (uint64_t)min(q, n - 1) * stride;
-      d.l = slen;
-    } else {
-      wave_desc<G>(off, len, q, n, d.o, d.l);
-    }
-    if (q >= n) d.l = 0;
-    d.sd = seed ? wave_u32<G>(seed, q, n) : 0u;  // uniform branch, scalar loads only
-    d.lp = kParity ? parity[min(q, n - 1)] : 0u;
-    return d;
-  };
-  // the packet's sum, stored; spans longer than G * U chunks finish with the
-  // serial rounds of Span (their later loads wait, as in k_spans)
-  auto done = [&](const SpanPP<G, U>& sp, uint32_t q, const Desc& d) {
-    uint64_t acc = sp.sum(lut, gl);
-    if (sp.end > 16 * kChunks) {
-      Span<G, U> rest;
-      rest.init(base + d.o, d.l);
-      acc += rest.rest_lut(lut, gl);
-    }
-    uint32_t x = fold16(acc);
-    if ((d.lp ^ (uint32_t)reinterpret_cast<uintptr_t>(base + d.o)) & 1) x = rot8(x);
-    x = group_sum<G>(x);
-    if (gl == 0 && q < n) out[q] = finish((uint64_t)x + d.sd, flags);
-  };
-  SpanPP<G, U> A, B;
-  Desc dA = desc(p);
-  A.load(base, dA.o, dA.l, gl);
-  lut.init();  // every thread reaches this barrier: no exit before it
-  if (__ballot(p < n) == 0) return;  // the whole wave is past the end
-  Desc dB = desc(p + S);
-  for (;;) {
-    B.load(base, dB.o, dB.l, gl);  // packet p + S in flight while p is summed
-    const Desc dC = desc(p + 2 * S);
-    done(A, p, dA);
-    if (__ballot(p + S < n) == 0) break;
-    A.load(base, dC.o, dC.l, gl);  // packet p + 2S in flight while p + S is summed
-    const Desc dD = desc(p + 3 * S);
-    done(B, p + S, dB);
-    if (__ballot(p + 2 * S < n) == 0) break;
-    p += 2 * S;
-    dA = dC;
-    dB = dD;
-  }
-}
+// k_spans_pp (round 2's default: two packets in flight per lane group, 54
+// vector instructions per KiB) was removed in round 3: k_spans_lean replaced
+// it (profiles/r03/pruned/spans_pp.diff).
 
 struct Geometry {
   int g, u;
@@ -288,7 +174,7 @@ struct Geometry {
 // unrolled round per packet with most lanes holding a chunk (1500 B -> 32
 // lanes x 3 loads = 96 chunks >= the 95 a 1500-B span can touch).
 Geometry pick_geometry(uint32_t mean_len) {
-  if (mean_len == 0) return {64, 2};
+  if (mean_len == 0) return {64, 3};  // unknown: any length, the lean kernel's rounds
   if (mean_len <= 64) return {4, 2};  // 16 packets per wave; an unaligned 64-B span spans 5 chunks
   if (mean_len <= 96) return {8, 1};
   if (mean_len <= 224) return {8, 2};
@@ -356,46 +242,17 @@ int blocks_per_cu(int dflt) {
 //     descriptors, mask-free whole chunks -- 23 VALU instructions per KiB,
 //     no power-ramp dip in the driver's window (profiles/r03/r03d/); at 4
 //     lanes per packet (mean length <= 64 B) k_spans_quad;
-//   2 k_spans_pp: round 2's default, kept for A/B (1-2 % faster warm, 53.7
-//     VALU / KiB, dips to 0.79 of peak late in the driver's window);
 //   0 k_spans: one packet per lane group, one-shot grid.
-// Geometries other than 32 x 3 / 64 x 3 (the spans_geo override) use k_spans_pp
-// under 1 and 2.
-// k_spans_pp at G x U (spans_pipe 2, wide descriptors only).
-static int launch_spans_pp(const void* base, const uint64_t* off, const uint32_t* len,
-                           const uint32_t* seed, const uint8_t* parity, uint16_t* out,
-                           uint32_t n, uint32_t flags, Geometry geo, hipStream_t stream) {
-  const int grid = grid_for(n, geo.g, 128);
-#define LP(G, U)                                                                          \
-  if (parity)                                                                             \
-    hipLaunchKernelGGL((k_spans_pp<G, U, true>), dim3(grid), dim3(kBlock), 0, stream,      \
-                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
-                       flags, (uint32_t)tuning().xcd_remap);                               \
-  else                                                                                    \
-    hipLaunchKernelGGL((k_spans_pp<G, U, false>), dim3(grid), dim3(kBlock), 0, stream,     \
-                       static_cast<const uint8_t*>(base), off, len, seed, parity, out, n,  \
-                       flags, (uint32_t)tuning().xcd_remap)
-  switch (geo.g * 16 + geo.u) {
-    case 32 * 16 + 3: LP(32, 3); break;
-    case 64 * 16 + 2: LP(64, 2); break;
-    default: LP(64, 3); break;
-  }
-#undef LP
-  return check_launch();
-}
-
-// Packed descriptors (uinet_cksum_spans32) take the same kernels; under
-// spans_pipe 2 (k_spans_pp, an A/B knob built for wide descriptors only) they
-// take the one-shot k_spans of spans_pipe 0.
+// Geometries of 8 and 16 lanes, and 64 x 2 (the spans_geo override), take
+// k_spans under both.  (2 was round 2's k_spans_pp, removed in round 3.)
+// Packed descriptors (uinet_cksum_spans32) take the same kernels.
 template <typename OffT, typename LenT>
 static int launch_spans_t(const void* base, const OffT* off, const LenT* len,
                           const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                           uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
-  constexpr bool kWide = sizeof(OffT) == 8;
   const Geometry geo = geometry_override(pick_geometry(len_hint));
-  int pipe = tuning().spans_pipe;
-  if (!kWide && pipe == 2) pipe = 0;
+  const int pipe = tuning().spans_pipe;
   // Scalar descriptors (G >= 32, knob "spans_sdesc", default on): a wave's
   // 1-2 packets' off / len come from s_loads, and the grid drops to one packet
   // per group (512 blocks per CU at 1 M x 1500 B).  Interleaved A/B, config 2
@@ -409,10 +266,6 @@ static int launch_spans_t(const void* base, const OffT* off, const LenT* len,
   if (sdesc && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, false, 0, 0,
                              tuning().blocks_per_cu, stream);
-  if constexpr (kWide) {
-    if (sdesc && pipe) return launch_spans_pp(base, off, len, seed, parity, out, n, flags, geo,
-                                              stream);
-  }
   const int grid = grid_for(n, geo.g, sdesc ? 512 : 256);
 #define L(G, U)                                                                          \
   if (sdesc && (G) >= 32)                                                                \
@@ -458,23 +311,6 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
     return launch_spans_lean<uint64_t, uint32_t>(base, nullptr, nullptr, seed, nullptr, out, n,
                                                  flags, geo.g, true, pkt_stride, len,
                                                  tuning().blocks_per_cu, stream);
-  if (geo.g >= 32 && pipe) {
-    // the persistent two-in-flight groups of k_spans_pp, descriptors from
-    // the stride: as for the span API, the one-shot grid (spans_pipe = 0)
-    // slows under the platform's power limit (profiles/r02/ab_strided_pp/)
-    const int grid = grid_for(n, geo.g, 128);
-#define LS(G, U)                                                                           \
-  hipLaunchKernelGGL((k_spans_pp<G, U, false, true>), dim3(grid), dim3(kBlock), 0, stream, \
-                     static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, out, n, \
-                     flags, (uint32_t)tuning().xcd_remap, pkt_stride, len)
-    switch (geo.g * 16 + geo.u) {
-      case 32 * 16 + 3: LS(32, 3); break;
-      case 64 * 16 + 2: LS(64, 2); break;
-      default: LS(64, 3); break;
-    }
-#undef LS
-    return check_launch();
-  }
   // one packet per group suits long packets; small ones want groups that
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
   const int grid = grid_for(n, geo.g, len <= 96 ? 256 : 4096);

@@ -172,12 +172,13 @@ def test_set_tuning_validation():
           ("chains_long", 16), ("chains_tile", 8), ("xcd_remap", 0), ("host_threads", 64),
           ("walk_prefetch", 0), ("walk_prefetch", 2), ("spans_geo", 0), ("spans_geo", 32 * 16 + 3),
           ("spans_sdesc", 0), ("host_group", 4), ("host_pin", 1), ("multi_gather", 1),
-          ("spans_pipe", 0), ("spans_pipe", 2)]
-    # chains_variant, spans_lut and spans_contig were removed in round 3
+          ("spans_pipe", 0), ("spans_pipe", 1)]
+    # chains_variant, spans_lut, spans_contig and spans_pipe 2 (k_spans_pp)
+    # were removed in round 3
     bad = [("blocks_per_cu", -1), ("chains_pass", 3), ("chains_pass", 8), ("chains_long", 15),
            ("chains_tile", 64), ("xcd_remap", 2), ("host_threads", 0), ("walk_prefetch", 3),
            ("spans_geo", 16 * 16 + 6), ("spans_geo", 5), ("spans_sdesc", 2), ("host_group", 0),
-           ("host_pin", 2), ("multi_gather", 2), ("spans_pipe", 3), ("chains_variant", 0),
+           ("host_pin", 2), ("multi_gather", 2), ("spans_pipe", 2), ("spans_pipe", 3), ("chains_variant", 0),
            ("spans_lut", 1), ("spans_contig", 0), ("no_such_knob", 1)]
     try:
         for k, v in ok:
