@@ -1,9 +1,7 @@
 #!/usr/bin/env bash
-# Round 3: chain kernel with the packed 16-bit key (segment pair minus chunk
-# position, clamped by packed ops, index and bin by one v_dot2), two
-# ds_bpermutes per chunk instead of three, ds_sub_u64 for the telescoping bin.
-# Chain parity tests on the new build, then base vs new in alternating bench
-# processes (tools/ab_lib_swap.sh) on configs 3, 3tx, 5tso.
+# Round 3: a chain-kernel change (base.so vs new.so in tools/ab_so/):
+# chain parity tests on the new build, then base vs new in alternating
+# bench processes (tools/ab_lib_swap.sh) on configs 3, 3tx, 5tso.
 set -u
 TAG=${TAG:-r03s2c}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
