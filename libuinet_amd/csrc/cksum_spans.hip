@@ -9,8 +9,9 @@
 // What it changes is the vector work per byte.  A streaming read that also
 // issues ~64 vector instructions per 16-B chunk and lane makes the platform
 // throttle 10-20 launches into a burst, one with ~32 does not
-// (profiles/r02/cold_ab/ section 4); k_spans_pp issued ~42 per KiB, most of
-// them per packet, not per byte.  Here every per-packet quantity is
+// (profiles/r02/cold_ab/ section 4); round 2's k_spans_pp (removed, see
+// profiles/r03/pruned/) issued ~42 per KiB, most of them per packet, not per
+// byte.  Here every per-packet quantity is
 // wave-uniform scalar work and the per-packet vector work is shared:
 //
 //  * Descriptors.  A wave folds kP = 64 / G packets per step (one per lane
@@ -34,7 +35,7 @@
 //    each 16-lane row then holds one packet's total, and the fold, the
 //    rotation (a shift by 0 or 8 and one more fold), the seed, the complement
 //    and the store run once for 2 (G = 64) or 4 (G = 32) packets.
-//  * Pipelining as in k_spans_pp: step k + 1's chunks are loaded before step
+//  * Pipelining: step k + 1's chunks are loaded before step
 //    k is summed, every load unconditional, so the wait for step k leaves step
 //    k + 1's loads in flight.  Spans longer than one round (16 G U bytes)
 //    finish with serial rounds.
