@@ -191,6 +191,10 @@ def dispatched_kernel(cfg: str, api: str, w) -> str:
     pipe = int(os.environ.get("UINET_CKSUM_SPANS_PIPE", "1") or 1)
     geo = int(os.environ.get("UINET_CKSUM_SPANS_GEO", "0") or 0)
     mean = w["length"] if api == "strided" else w["hint"]
+    if (api == "strided" and pipe == 1 and not geo and 32 <= w["stride"] <= 256
+            and w["length"] <= w["stride"] and 4 * (w["stride"] - w["length"]) <= w["stride"]
+            and (w["base"] | w["stride"]) % 16):
+        return "k_strided_dense"  # launch_strided: small packets off 16-B alignment
     g = 4 if mean <= 64 else 8 if mean <= 224 else 16 if mean <= 720 else 32 if mean <= 1520 else 64
     u = 2 if g == 4 else 3
     if api == "strided" and mean <= 64 and (w["base"] | w["stride"]) % 16 == 0:

@@ -66,6 +66,12 @@ int launch_spans_quad(const void* base, const OffT* off, const LenT* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int u, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream);
+// k_strided_dense (cksum_spans.hip): small strided packets laid nearly back
+// to back (32 <= stride <= 256, stride - len <= stride / 4); returns 1 without
+// launching when the shape does not fit.
+int launch_strided_dense(const void* base, uint64_t stride, uint32_t len, const uint32_t* seed,
+                         uint16_t* out, uint32_t n, uint32_t flags, int blocks_cu,
+                         hipStream_t stream);
 int launch_chains(const void* base, const uint64_t* seg_off, const uint32_t* seg_len,
                   const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                   const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
