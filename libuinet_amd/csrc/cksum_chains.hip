@@ -361,10 +361,16 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
         if (pend) consume(va, ka);  // drain at the end of the round
         pend = 0;
       };
+#ifdef UINET_CHAINS_LAB_NOLIST  // tools/chains ablation only: descriptor rounds, no chunk list
+      (void)run;
+      if ((r16 ^ mval ^ dkr ^ (uint32_t)dk ^ (uint32_t)window ^ C) == 0x9e3779b9u)
+        atomicAdd(&acc[lane], 1ull);
+#else
       if (window)
         run(std::true_type());
       else
         run(std::false_type());
+#endif
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (lane < np) {
