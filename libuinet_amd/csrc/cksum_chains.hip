@@ -50,7 +50,7 @@ constexpr int kWaves = kBlock / 64;
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short us16x2 __attribute__((ext_vector_type(2)));
 #ifndef UINET_CHAINS_LONGU  // build-time A/B knob (profiles/r01/ab/chains_occ/longu)
-#define UINET_CHAINS_LONGU 4
+#define UINET_CHAINS_LONGU 2
 #endif
 constexpr int kLongU = UINET_CHAINS_LONGU;  // chunks in flight per lane on a long segment
 constexpr uint32_t kListMax = 1024;  // longest segment (chunks) the chunk list takes
@@ -88,16 +88,19 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 // temporal instead of non-temporal loads (HBM bytes -1.1 %, time +8 %), an
 // XCD-banded tile order, smaller tiles at the end of the launch, a pipelined
 // long-segment stream (profiles/r01/ab/).
-// Build-time occupancy override for A/B (-DUINET_CHAINS_WAVES=7|8 forces that
-// many waves per SIMD, spilling what does not fit); unset = the compiler's 80
-// VGPRs, occupancy 6.
-// The default holds the kPass = 2 kernel at 6 waves per SIMD (80 VGPRs, no
+// Build-time occupancy override for A/B (-DUINET_CHAINS_WAVES=N forces that
+// many waves per SIMD, spilling what does not fit).
+// The default holds the kPass = 2 kernel at 7 waves per SIMD (72 VGPRs, no
 // spills): left alone the compiler takes 88 for the interleaved consume and
-// drops to 5.
+// drops to 5.  7 fits because a long segment keeps 2 chunks per lane in flight
+// (kLongU), not 4: the long-segment loads were the round-level pressure point
+// that spilled 36 B at 7 waves (profiles/r03/r03s2d/).  7 waves with kLongU 2
+// against 6 with 4: config 3 -1.0 %, 3tx -0.2 %, 5tso -0.7 % time
+// (profiles/r03/r03s2u/); 8 waves (64 VGPRs) still spills, +21 %.
 #ifdef UINET_CHAINS_WAVES
 #define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(UINET_CHAINS_WAVES)))
 #else
-#define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(kPass == 2 ? 6 : 1)))
+#define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(kPass == 2 ? 7 : 1)))
 #endif
 
 template <int kPass, int kTile, typename OffT, typename LenT>
