@@ -210,10 +210,49 @@ def dispatched_kernel(cfg: str, api: str, w) -> str:
     return "k_spans"
 
 
+# The sources each kernel family is compiled from: a FETCH_SIZE entry counts
+# only while they are byte-identical to the ones it was measured on.
+KERNEL_SOURCES = {
+    "k_chains_pipe": ("cksum_chains.hip", "cksum_device.h"),
+    "k_spans_lean": ("cksum_spans.hip", "cksum_device.h"),
+    "k_spans_quad": ("cksum_spans.hip", "cksum_device.h"),
+    "k_strided_dense": ("cksum_spans.hip", "cksum_device.h"),
+    "k_spans": ("cksum_kernels.hip", "cksum_device.h"),
+}
+
+
+def short_kernel(name: str) -> str:
+    """A demangled kernel name as tools/pmc_summary.py keys it:
+    'k_chains_pipe<2,32,2,unsignedlong,unsignedint>'."""
+    import re
+
+    m = re.search(r"(k_\w+)<([^>]*)>", name)
+    if m:
+        return f"{m.group(1)}<{m.group(2).replace(' ', '')}>"
+    return name.split("(")[0][-60:]
+
+
+def kernel_src_sha(kernel: str):
+    """sha256 (16 hex digits) of the sources the kernel (short or family
+    name) is built from; None for an unknown family."""
+    import hashlib
+
+    fam = kernel.split("<")[0]
+    files = KERNEL_SOURCES.get(fam)
+    if files is None:
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(REPO, "libuinet_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_traffic(path: str, key: str, kernel: str):
     """HBM bytes per launch from the FETCH_SIZE passes folded into `path`
-    (tools/prof_all.sh), with where they were measured; None when the entry
-    was measured on a different kernel than the one this line launched."""
+    (tools/prof_all.sh), with where they were measured.  None unless the
+    entry was measured on exactly this instantiation (`kernel`, the short name
+    of what the engine launched) built from today's sources."""
     try:
         with open(path) as f:
             e = json.load(f).get(key)
@@ -221,9 +260,13 @@ def load_traffic(path: str, key: str, kernel: str):
         e = None
     if e is None:
         return None, {"key": key, "note": "no FETCH_SIZE entry"}
-    src = {"key": key, "source": e.get("source"), "measured_kernel": e.get("kernel")}
-    if not str(e.get("kernel", "")).startswith(kernel + "<"):
+    src = {"key": key, "source": e.get("source"), "measured_kernel": e.get("kernel"),
+           "launched_kernel": kernel}
+    if e.get("kernel") != kernel:
         src["note"] = "measured on another kernel: not reported"
+        return None, src
+    if e.get("src_sha") is None or e.get("src_sha") != kernel_src_sha(kernel):
+        src["note"] = "measured on an older build of this kernel: not reported"
         return None, src
     return float(e["hbm_read_bytes_per_launch"]), src
 
@@ -332,7 +375,7 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
         timer = (lambda nt, cp, r: R.time_skip(*args, nthreads=nt, cpus=cp, reps=r)) if R else None
         port = lambda: oracle.Oracle().skip_batch(*args, nthreads=threads)  # noqa: E731
     gib = w["bytes"] / 2**30
-    runs = {}
+    runs, spread = {}, {}
     if timer is not None:
         # median of 5 single passes per (threads, placement): the threads pinned
         # to the first CPUs of the process mask, and left to the scheduler (on
@@ -348,6 +391,7 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
                 rr = [timer(nt, cpus[:nt] if placement == "pinned" else None, 1)
                       for _ in range(5)]
                 runs[f"{nt}_{placement}"] = float(np.median([r[0] for r in rr]))
+                spread[f"{nt}_{placement}"] = (min(r[0] for r in rr), max(r[0] for r in rr))
                 outs.append(rr[-1][1])
         best = min((k for k in runs if k.startswith(f"{threads}_")), key=runs.get)
         tn = runs[best]
@@ -356,8 +400,13 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
         t0 = time.perf_counter(); o = port(); t1 = time.perf_counter() - t0  # noqa: E702
         outs, tn, best = [o], t1, f"{threads}_port"
         runs[best] = t1
+        spread[best] = (t1, t1)
     parity = bool(all(np.array_equal(o, gpu_out) for o in outs))
     rates = {k: round(gib / t, 3) for k, t in runs.items()}
+    # min / max GiB/s of the 5 passes: the many-thread figure swings by 4x
+    # from box to box (64.8 .. 271.2 GiB/s for one command on one CPU model,
+    # VERDICT r03); the 1-thread figure is the stable comparison
+    minmax = {k: [round(gib / hi, 3), round(gib / lo, 3)] for k, (lo, hi) in spread.items()}
     return {
         "value": round(gib / tn, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
         "cpu_model": cpu_model(),
@@ -365,9 +414,12 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
                    f"host copy as {'chained ' if cfg in CHAIN_CONFIGS else ''}struct mbuf; median "
                    f"of 5 passes per thread count and placement (GiB/s: "
                    + ", ".join(f"{k.replace('_', ' threads ')} {v}" for k, v in rates.items())
-                   + f"); value = {best.replace('_', ' threads ')}; results bit-identical to "
+                   + f"); value = {best.replace('_', ' threads ')} (its 5 passes: "
+                   + "{}-{} GiB/s".format(*minmax[best])
+                   + f"; the 1-thread figure is the stable comparison); results bit-identical to "
                    f"the GPU in every run: {parity}"),
         "runs_gibs": rates,
+        "runs_minmax_gibs": minmax,
         "value_from": best,
         "placement": best.split("_")[1],
         "one_thread_gibs": round(gib / t1, 3),
@@ -387,6 +439,31 @@ def main():
                  f"torchrun --nproc-per-node {args.gpus} (or drop the launcher)")
     if args.config is None:
         args.config = "4" if distributed else "2"
+    # N > 1: every phase has a deadline (libuinet_amd.dist.Watchdog).  A rank
+    # stuck in the rendezvous, RCCL init, a step or the parity gather -- or
+    # failing in one -- prints one JSON line naming the phase and exits
+    # non-zero, instead of leaving the launcher to kill a silent run.
+    wd = None
+    if distributed:
+        from libuinet_amd.dist import Watchdog
+
+        wd = Watchdog(int(os.environ.get("RANK", "0")))
+    try:
+        run(args, distributed, wd)
+    except Exception as e:
+        if wd is None:
+            raise
+        import traceback
+
+        traceback.print_exc()
+        wd.fail(e)
+
+
+def run(args, distributed: bool, wd):
+    def phase(name):
+        if wd is not None:
+            wd.enter(name)
+
     import torch
     import torch.distributed as dist
 
@@ -394,7 +471,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
         if distributed:
+            phase("rendezvous")
             dist.init_process_group("gloo")
+            phase("plan")
         plan = {"rank": rank, "local_rank": local,
                 "world": dist.get_world_size() if distributed else 1, "config": args.config,
                 "packets_per_gpu": args.packets or {"4": 1 << 21, "2s": 1 << 24, "2su": 1 << 24,
@@ -402,7 +481,10 @@ def main():
                 "backend": os.environ.get("UINET_BENCH_BACKEND", "nccl") if distributed else None}
         print(json.dumps(plan), flush=True)
         if distributed:
+            dist.barrier()
+            phase("teardown")
             dist.destroy_process_group()
+            wd.done()
         return
     # UINET_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
     # one GPU (CI / 1-GPU boxes); the real runs use RCCL, one rank per GPU.
@@ -412,6 +494,7 @@ def main():
         sys.exit(f"bench: rank {rank} has LOCAL_RANK {local} but {ndev} GPU(s) are visible "
                  "(RCCL needs one GPU per rank; UINET_BENCH_BACKEND=gloo shares one)")
     dev = local % max(1, ndev)
+    phase("rendezvous")
     torch.cuda.set_device(dev)
     if distributed:
         if backend == "nccl":
@@ -425,6 +508,7 @@ def main():
 
     if not u.device_ok():
         raise SystemExit("bench: no gfx950 device visible")
+    phase("workload")
     w = build_workload(args.config, args.packets, rank, world)
     n = w["n"]
     # three result buffers (N > 1): step k's gather is enqueued after step
@@ -488,11 +572,13 @@ def main():
             rg.start(outs[i_last % NBUF], i_last % NBUF)
             rg.wait_all()
 
+    phase("warmup")
     for i in range(Wm):
         step(None, i)
     if Wm:
         drain(Wm - 1)
     torch.cuda.synchronize()
+    phase("timed")
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -519,14 +605,16 @@ def main():
     else:
         kms = np.array([ev[0][0].elapsed_time(ev[0][1]) / K])  # mean ms per launch
 
+    phase("parity")
     result = None
     if rank == 0:
         total_bytes = w["bytes"] * world * K
         value = total_bytes / elapsed / 2**30
         achieved = w["bytes"] / (kms.mean() * 1e-3) / 1e9
         key = f"{kernel_name(args.config, args.api, args.desc)}:config{args.config}:{n}"
-        kern = dispatched_kernel(args.config, args.api, w)
-        traffic, traffic_src = load_traffic(args.pmc, key, kern)
+        launched = short_kernel(u.last_kernel())  # the instantiation that really ran
+        kern = launched.split("<")[0] or dispatched_kernel(args.config, args.api, w)
+        traffic, traffic_src = load_traffic(args.pmc, key, launched)
         result = {
             "metric": metric_name(),
             "value": round(value, 3),
@@ -557,6 +645,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": kern,
+                "instance": launched,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -606,8 +695,10 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:
+        phase("teardown")
         dist.barrier()
         dist.destroy_process_group()
+        wd.done()
 
 
 def host_path_rate(args, w):

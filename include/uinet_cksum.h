@@ -134,6 +134,10 @@ int in6_cksum_pseudo(struct ip6_hdr *ip6, uint32_t len, uint8_t nxt,
 
 /* Engine version string and HIP diagnostics. */
 const char *uinet_cksum_version(void);
+/* The kernel instantiation (demangled, e.g. "void uinet::(anonymous
+ * namespace)::k_chains_pipe<2, 32, 2, unsigned long, unsigned int>(...)")
+ * the calling thread's last launch started; "" before the first launch. */
+const char *uinet_cksum_last_kernel(void);
 const char *uinet_cksum_strerror(int code);
 int uinet_cksum_last_hip_error(void);
 /* 1 when a gfx950 device is visible to the calling thread, else 0. */
@@ -375,8 +379,9 @@ struct uinet_cksum_shard {
  * root_out. */
 int uinet_cksum_spans_multi(const struct uinet_cksum_shard *shards, int nshards,
     uint32_t flags, uint32_t len_hint, int root_device, uint16_t *root_out);
-/* How the calling thread's last uinet_cksum_spans_multi gathered: 1 RCCL,
- * 0 peer copies, -1 no call yet. */
+/* How the calling thread's last uinet_cksum_spans_multi gathered: 1 RCCL
+ * (also when that call failed inside the RCCL path), 0 peer copies, -1 no
+ * call yet or the last call was rejected before any gather. */
 int uinet_cksum_multi_last_gather(void);
 
 /* A host-mbuf batch (in_cksum_skip_batch semantics) over ndev devices: the

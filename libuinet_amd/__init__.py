@@ -46,7 +46,7 @@ OK, EINVAL, ENODEV, ENOMEM, EHIP = 0, -22, -19, -12, -5
 EXPORTED_SYMBOLS = (
     "in_cksum_skip", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo", "in_addword",
     "uinet_cksum_version", "uinet_cksum_strerror", "uinet_cksum_last_hip_error",
-    "uinet_cksum_device_ok", "uinet_cksum_set_tuning", "uinet_cksum_spans", "uinet_cksum_spans32",
+    "uinet_cksum_last_kernel", "uinet_cksum_device_ok", "uinet_cksum_set_tuning", "uinet_cksum_spans", "uinet_cksum_spans32",
     "uinet_cksum_strided", "uinet_cksum_chains", "uinet_cksum_chains32",
     "in_cksum_skip_batch", "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch",
     "uinet_cksum_register_host", "uinet_cksum_unregister_host",
@@ -96,6 +96,7 @@ def lib() -> ctypes.CDLL:
         "in_pseudo": (ctypes.c_ushort, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]),
         "in_addword": (ctypes.c_ushort, [ctypes.c_ushort, ctypes.c_ushort]),
         "uinet_cksum_version": (ctypes.c_char_p, []),
+        "uinet_cksum_last_kernel": (ctypes.c_char_p, []),
         "uinet_cksum_strerror": (ctypes.c_char_p, [_i32]),
         "uinet_cksum_last_hip_error": (_i32, []),
         "uinet_cksum_device_ok": (_i32, []),
@@ -459,6 +460,12 @@ def in_cksum_skip_batch_multi(devices, heads, length, skip) -> np.ndarray:
 def set_tuning(key: str, value: int) -> None:
     """uinet_cksum_set_tuning: performance knobs that never change results."""
     _check("uinet_cksum_set_tuning", lib().uinet_cksum_set_tuning(key.encode(), value))
+
+
+def last_kernel() -> str:
+    """The kernel instantiation this thread's last launch started (demangled;
+    "" before any launch): uinet_cksum_last_kernel."""
+    return lib().uinet_cksum_last_kernel().decode()
 
 
 def device_ok() -> bool:

@@ -26,11 +26,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cxxabi.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <mutex>
 #include <shared_mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -52,13 +55,16 @@ int record_hip(hipError_t e) {
 
 int check_launch() { return record_hip(hipGetLastError()); }
 
+thread_local const void* t_last_kernel = nullptr;
+void note_kernel(const void* host_stub) { t_last_kernel = host_stub; }
+
 // The live knob values.  uinet_cksum_set_tuning may run while other threads
 // launch, so each knob is a relaxed atomic and a launch reads one snapshot
 // (tuning()).  The environment seeds them through the same validation.
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_pass{2}, host_threads{8}, chains_long{128},
       chains_tile{0}, xcd_remap{1}, walk_prefetch{1}, spans_geo{0}, spans_sdesc{1},
-      spans_pipe{1}, host_group{1}, host_pin{0}, multi_gather{0};
+      spans_pipe{1}, host_group{1}, host_pin{0}, multi_gather{0}, chains_sweep{2};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -83,6 +89,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"host_group", &TuningLive::host_group, [](int v) { return v >= 1 && v <= 64; }},
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
+      {"chains_sweep", &TuningLive::chains_sweep, [](int v) { return v == 0 || v == 2 || v == 4; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -102,6 +109,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_SPANS_SDESC", "spans_sdesc"},
         {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},       {"UINET_CKSUM_HOST_GROUP", "host_group"},
         {"UINET_CKSUM_HOST_PIN", "host_pin"},          {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},
+        {"UINET_CKSUM_CHAINS_SWEEP", "chains_sweep"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -133,6 +141,7 @@ Tuning tuning() {
   x.host_group = ld(t.host_group);
   x.host_pin = ld(t.host_pin);
   x.multi_gather = ld(t.multi_gather);
+  x.chains_sweep = ld(t.chains_sweep);
   return x;
 }
 
@@ -838,6 +847,19 @@ using namespace uinet;
 extern "C" {
 
 const char* uinet_cksum_version(void) { return "libuinet_cksum 0.1 (gfx950)"; }
+
+const char* uinet_cksum_last_kernel(void) {
+  thread_local std::string name;
+  name.clear();
+  if (!t_last_kernel) return "";
+  const char* m = hipKernelNameRefByPtr(t_last_kernel, nullptr);
+  if (!m) return "";
+  int st = 0;
+  char* d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+  name = (st == 0 && d) ? d : m;
+  free(d);
+  return name.c_str();
+}
 
 const char* uinet_cksum_strerror(int code) {
   switch (code) {

@@ -103,7 +103,19 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 #define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(kPass == 2 ? 7 : 1)))
 #endif
 
-template <int kPass, int kTile, typename OffT, typename LenT>
+// kSweep > 0 adds the address sweep (a descriptor round whose list segments
+// lie inside one dense address range, e.g. mbufs carved in order out of one
+// buffer): the wave reads that range as plain 16-B chunks, kSweep passes of
+// 64 per window, with no per-chunk segment lookup, mask or bin.  Each chunk
+// adds its whole 8-halfword sum to a running prefix F (one DPP scan per pass);
+// F and the chunk are staged in LDS for the window, and each segment's lane
+// reads, in the window holding its first and its last kept byte,
+//   F(x) = F(first byte of x's chunk) + (halves of x's chunk below x)
+// so the segment's sum is F(end) - F(start) (exact modulo 2^32: a list segment
+// is < 16 KiB, its weighted sum < 2^29).  One u64 LDS atomic per segment puts
+// it into its (packet, parity) bin.  Rounds that do not qualify (segments
+// scattered over more than 1.25x their own chunks) take the chunk list below.
+template <int kPass, int kTile, int kSweep, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
                                                        const LenT* __restrict__ seg_len,
@@ -123,6 +135,9 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
   // segment-start markers per batch, (lane + 1) << 8 | meta, and one spare slot
   // per lane that lanes without a start in the batch write (no exec mask)
   __shared__ uint16_t lds_mark[kWaves][kWin + 64];
+  constexpr int kSwCh = 64 * (kSweep > 0 ? kSweep : 1);  // chunks per sweep window
+  __shared__ u32x4 lds_swd[kSweep > 0 ? kWaves : 1][kSweep > 0 ? kSwCh : 1];   // window bytes
+  __shared__ uint32_t lds_swf[kSweep > 0 ? kWaves : 1][kSweep > 0 ? kSwCh : 1];  // F per chunk
   lut.init();
   for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
   for (int i = threadIdx.x; i < kWaves * (kWin + 64); i += blockDim.x) (&lds_mark[0][0])[i] = 0;
@@ -277,6 +292,70 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint64_t lm_list = __ballot(nch_l != 0);
       if (lm_list == 0) continue;
       const int lf = (int)__builtin_ctzll(lm_list);
+      // --- the address sweep ------------------------------------------------
+      if constexpr (kSweep > 0) {
+        const bool li = nch_l != 0;
+        const uint64_t a_abs = reinterpret_cast<uintptr_t>(base) + ao;  // first kept byte
+        const uint64_t a_end = a_abs + eff - 1;                         // last kept byte
+        const uint64_t X0 = readlane_u64((uint32_t)(a_abs >> 4), (uint32_t)(a_abs >> 36), lf);
+        // chunk numbers relative to the first list segment's, biased by 2^24:
+        // the round qualifies only if every one lies within 2^24 chunks of it
+        const uint64_t ds = (a_abs >> 4) - X0 + (1ull << 24);
+        const uint64_t de = (a_end >> 4) - X0 + (1ull << 24);
+        const bool inr = !li || (ds < (1ull << 25) && de < (1ull << 25));
+        const uint32_t rs = li ? (uint32_t)ds : 0xffffffffu;
+        const uint32_t re = li ? (uint32_t)de : 0u;
+        const uint32_t mn = ~readlane_u32(wave_scan<1, false>(~rs, 0u), 63);
+        const uint32_t mx = readlane_u32(wave_scan<1, false>(re, 0u), 63);
+        const uint32_t span = mx - mn + 1u;  // chunks of the range (valid when all inr)
+        if (__ballot(!inr) == 0 && span <= C + (C >> 2) + 64u) {
+          const uint64_t sb = (X0 + mn - (1ull << 24)) << 4;  // the range's first chunk
+          const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+              reinterpret_cast<void*>(sb), 0, (int)(16u * span), 0x00020000);
+          // window-relative chunk of the first / last kept byte (lanes without
+          // a list segment: never in a window), and the byte bounds there
+          const uint32_t sc = li ? rs - mn : 0xffffffffu;
+          const uint32_t ec = li ? re - mn : 0xffffffffu;
+          const uint32_t hb = (uint32_t)a_abs & 15u;        // bytes below the first
+          const uint32_t tb = ((uint32_t)a_end & 15u) + 1u;  // bytes up to the last
+          u32x4* swd = lds_swd[wid];
+          uint32_t* swf = lds_swf[wid];
+          u32x4 v[kSweep];
+          // chunks past the range read 0 (buffer range check): no clamp, no fault
+          auto sweep_load = [&](uint32_t w0) {
+#pragma unroll
+            for (int q = 0; q < kSweep; ++q)
+              v[q] = __builtin_amdgcn_raw_buffer_load_b128(
+                  sr, (int)(16u * (w0 + (uint32_t)(q * 64 + lane))), 0, 2);
+          };
+          uint32_t seg = 0;    // F(end) - F(start), modulo 2^32
+          uint32_t fbase = 0;  // F at the window's first chunk
+          sweep_load(0);
+          for (uint32_t w0 = 0; w0 < span; w0 += (uint32_t)kSwCh) {
+            uint32_t s[kSweep], I[kSweep];
+#pragma unroll
+            for (int q = 0; q < kSweep; ++q) {
+              s[q] = chunk_halves(v[q], 0u);  // < 2^19
+              I[q] = s[q];
+            }
+            wave_scan_add_n<kSweep>(I);
+#pragma unroll
+            for (int q = 0; q < kSweep; ++q) {
+              swd[q * 64 + lane] = v[q];
+              swf[q * 64 + lane] = fbase + I[q] - s[q];
+              fbase += readlane_u32(I[q], 63);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (w0 + (uint32_t)kSwCh < span) sweep_load(w0 + (uint32_t)kSwCh);
+            const uint32_t js = sc - w0, je = ec - w0;
+            if (js < (uint32_t)kSwCh) seg -= chunk_halves_masked(swd[js], lut.m[hb], swf[js]);
+            if (je < (uint32_t)kSwCh) seg += chunk_halves_masked(swd[je], lut.m[tb], swf[je]);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          }
+          if (li) atomicAdd(&acc[meta], (unsigned long long)seg);
+          continue;
+        }
+      }
       const uint64_t R0 = readlane_u64(c0_lo, c0_hi, lf);
       const uint64_t rel = c0 - R0 + (1ull << 31);  // R0 - 2 GiB .. R0 + 2 GiB
       const bool window = __ballot(nch_l != 0 && rel >= (1ull << 32) - (1ull << 16)) == 0;
@@ -405,16 +484,23 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
-#define LF(P, T)                                                                           \
-  hipLaunchKernelGGL((k_chains_pipe<P, T, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0,   \
+#define LF(P, T, S)                                                                        \
+  UINET_LAUNCH((k_chains_pipe<P, T, S, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, \
                      stream, b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
+#define LFS(P, T)                        \
+  do {                                   \
+    if (tn.chains_sweep == 4) LF(P, T, 4); \
+    else if (tn.chains_sweep == 2) LF(P, T, 2); \
+    else LF(P, T, 0);                    \
+  } while (0)
   if (tile == 8) {
-    if (tn.chains_pass == 4) LF(4, 8);
-    else LF(2, 8);
+    if (tn.chains_pass == 4) LFS(4, 8);
+    else LFS(2, 8);
   } else {
-    if (tn.chains_pass == 4) LF(4, 32);
-    else LF(2, 32);
+    if (tn.chains_pass == 4) LFS(4, 32);
+    else LFS(2, 32);
   }
+#undef LFS
 #undef LF
   return check_launch();
 }

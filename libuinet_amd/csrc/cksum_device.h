@@ -86,6 +86,27 @@ __device__ __forceinline__ uint64_t chunk_sum(u32x4 v, int s, int e) {
   return masked_sum(v, chunk_mask(clampi(s, 0, 16), clampi(e, 0, 16)));
 }
 
+// Sum of the eight 16-bit halves of a chunk, plus acc: the exact integer sum
+// of its bytes weighted 256^(address & 1), one v_dot2_u32_u16 against (1, 1)
+// per word.  The words are copied out of the vector before the bit-cast:
+// hipcc (ROCm 7.2, gfx950) compiles __builtin_bit_cast(us2, v.y) taken
+// straight off an ext-vector ELEMENT as v.x in some contexts (one dword read
+// four times; tests/native/dot2_repro.hip reproduces it and
+// tests/test_dot2_isa.py checks this helper's code on every build).
+__device__ __forceinline__ uint32_t chunk_halves(u32x4 v, uint32_t acc) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  const us2 one = {1, 1};
+  const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, w0), one, acc, false);
+  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, w1), one, acc, false);
+  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, w2), one, acc, false);
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, w3), one, acc, false);
+}
+// The same over the bytes a mask keeps.
+__device__ __forceinline__ uint32_t chunk_halves_masked(u32x4 v, u32x4 m, uint32_t acc) {
+  return chunk_halves(v & m, acc);
+}
+
 // 17 x 17 table of chunk masks in LDS: entry s * 17 + e keeps bytes [s, e).
 // One ds_read_b128 replaces ~30 VALU instructions of shift/select per chunk.
 struct MaskLut {
@@ -114,12 +135,7 @@ struct MaskLut {
   // accumulator in one instruction: 4 AND + 4 dot2 per chunk, no carries
   // and no fold (the add-with-carry chain took 4 AND + 4 addc + 3 for the fold).
   __device__ static __forceinline__ uint32_t halves_sum(u32x4 v, u32x4 k) {
-    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const us2 one = {1, 1};
-    uint32_t t = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, v.x & k.x), one, 0u, false);
-    t = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, v.y & k.y), one, t, false);
-    t = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, v.z & k.z), one, t, false);
-    return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, v.w & k.w), one, t, false);
+    return chunk_halves_masked(v, k, 0u);
   }
 };
 

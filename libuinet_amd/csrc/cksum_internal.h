@@ -30,6 +30,7 @@ struct Tuning {
                        // group (a pool pass walks a group while the GPU folds the last)
   int host_pin;        // host pool helpers pinned to CPUs 1.. of the process mask (0/1)
   int multi_gather;    // uinet_cksum_spans_multi: 0 RCCL gather when it applies, 1 peer copies
+  int chains_sweep;    // chain kernel: address-sweep window in 64-chunk passes (2, 4), 0 = off
 };
 Tuning tuning();
 // True when G * 16 + U names a compiled span-kernel geometry.
@@ -39,6 +40,16 @@ bool span_geometry_ok(int code);
 // it to a UINET_CKSUM_* code.
 int check_launch();
 int record_hip(hipError_t e);
+
+// Every kernel launch goes through UINET_LAUNCH, which notes the kernel's
+// host stub for uinet_cksum_last_kernel() (the instantiation a launch on this
+// thread last started: bench.py matches its profiler traffic by that name).
+void note_kernel(const void* host_stub);
+#define UINET_LAUNCH(K, ...)                               \
+  do {                                                     \
+    ::uinet::note_kernel(reinterpret_cast<const void*>(&K)); \
+    hipLaunchKernelGGL(K, __VA_ARGS__);                    \
+  } while (0)
 
 int launch_spans(const void* base, const uint64_t* off, const uint32_t* len,
                  const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,

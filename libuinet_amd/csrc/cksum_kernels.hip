@@ -269,11 +269,11 @@ static int launch_spans_t(const void* base, const OffT* off, const LenT* len,
   const int grid = grid_for(n, geo.g, sdesc ? 512 : 256);
 #define L(G, U)                                                                          \
   if (sdesc && (G) >= 32)                                                                \
-    hipLaunchKernelGGL((k_spans<G, U, false, true, OffT, LenT>), dim3(grid), dim3(kBlock), \
+    UINET_LAUNCH((k_spans<G, U, false, true, OffT, LenT>), dim3(grid), dim3(kBlock), \
                        0, stream, static_cast<const uint8_t*>(base), off, len, seed, parity, \
                        0ull, 0u, out, n, flags, (uint32_t)tuning().xcd_remap);           \
   else                                                                                   \
-    hipLaunchKernelGGL((k_spans<G, U, false, false, OffT, LenT>), dim3(grid), dim3(kBlock), \
+    UINET_LAUNCH((k_spans<G, U, false, false, OffT, LenT>), dim3(grid), dim3(kBlock), \
                        0, stream, static_cast<const uint8_t*>(base), off, len, seed, parity, \
                        0ull, 0u, out, n, flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
@@ -324,7 +324,7 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
   const int grid = grid_for(n, geo.g, len <= 96 ? 256 : 4096);
 #define L(G, U)                                                                        \
-  hipLaunchKernelGGL((k_spans<G, U, true, false, uint64_t, uint32_t>), dim3(grid),      \
+  UINET_LAUNCH((k_spans<G, U, true, false, uint64_t, uint32_t>), dim3(grid),      \
                      dim3(kBlock), 0, stream,                                          \
                      static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
                      pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap)

@@ -106,6 +106,7 @@ struct Rccl {
   decltype(&ncclGather) gather = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
 };
 const Rccl& rccl() {
   static const Rccl r = [] {
@@ -117,7 +118,8 @@ const Rccl& rccl() {
     x.gather = reinterpret_cast<decltype(x.gather)>(dlsym(h, "ncclGather"));
     x.group_start = reinterpret_cast<decltype(x.group_start)>(dlsym(h, "ncclGroupStart"));
     x.group_end = reinterpret_cast<decltype(x.group_end)>(dlsym(h, "ncclGroupEnd"));
-    x.ok = x.init && x.gather && x.group_start && x.group_end;
+    x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.ok = x.init && x.gather && x.group_start && x.group_end && x.destroy;
     return x;
   }();
   return r;
@@ -129,7 +131,6 @@ const Rccl& rccl() {
 // use the same list serialise on its mutex.
 struct CommSet {
   std::mutex mu;
-  bool ok = false;
   std::vector<int> dev;
   std::vector<ncclComm_t> comm;
   std::vector<hipStream_t> stream;
@@ -138,25 +139,47 @@ struct CommSet {
   uint16_t* pad = nullptr;     // root: ranks x cap, for unequal shards
   uint64_t pad_cap = 0;
 };
+// A failed build releases what it made (communicators, streams) and is not
+// remembered, so a transient failure (a HIP error while another process holds
+// a device, a busy xGMI link) does not disable RCCL for the process: the next
+// call retries.  A device list that fails kMaxTries times, or whose failure
+// can only recur (RCCL rejects the arguments), falls back to peer copies at
+// once from then on.
+constexpr int kMaxTries = 3;
 CommSet* comm_set(const std::vector<int>& dev) {
   static std::mutex mu;
   static std::map<std::vector<int>, CommSet*>* sets = new std::map<std::vector<int>, CommSet*>;
+  static std::map<std::vector<int>, int>* fails = new std::map<std::vector<int>, int>;
   std::lock_guard<std::mutex> g(mu);
-  CommSet*& cs = (*sets)[dev];
-  if (cs) return cs->ok ? cs : nullptr;
-  cs = new CommSet;  // kept even when init fails: the next call falls back at once
+  auto it = sets->find(dev);
+  if (it != sets->end()) return it->second;
+  int& nfail = (*fails)[dev];
+  if (nfail >= kMaxTries) return nullptr;
+  auto* cs = new CommSet;
   cs->dev = dev;
   cs->comm.assign(dev.size(), nullptr);
-  if (rccl().init(cs->comm.data(), (int)dev.size(), dev.data()) != ncclSuccess) return nullptr;
   cs->stream.assign(dev.size(), nullptr);
   cs->buf.assign(dev.size(), nullptr);
-  for (size_t k = 0; k < dev.size(); k++) {
-    if (hipSetDevice(dev[k]) != hipSuccess ||
-        hipStreamCreateWithFlags(&cs->stream[k], hipStreamNonBlocking) != hipSuccess)
-      return nullptr;
+  const ncclResult_t r = rccl().init(cs->comm.data(), (int)dev.size(), dev.data());
+  bool ok = r == ncclSuccess;
+  for (size_t k = 0; ok && k < dev.size(); k++)
+    ok = hipSetDevice(dev[k]) == hipSuccess &&
+         hipStreamCreateWithFlags(&cs->stream[k], hipStreamNonBlocking) == hipSuccess;
+  if (ok) {
+    sets->emplace(dev, cs);
+    return cs;
   }
-  cs->ok = true;
-  return cs;
+  (void)hipGetLastError();
+  for (size_t k = 0; k < dev.size(); k++) {
+    if (cs->stream[k]) {
+      (void)hipSetDevice(dev[k]);
+      (void)hipStreamDestroy(cs->stream[k]);
+    }
+    if (cs->comm[k]) (void)rccl().destroy(cs->comm[k]);
+  }
+  delete cs;
+  nfail = (r == ncclInvalidArgument || r == ncclInvalidUsage) ? kMaxTries : nfail + 1;
+  return nullptr;
 }
 
 thread_local int t_last_gather = -1;  // 1 RCCL, 0 peer copies (uinet_cksum_multi_last_gather)
@@ -182,8 +205,19 @@ int spans_multi_rccl(const uinet_cksum_shard* shards, int ns, uint32_t flags, ui
   CommSet* cs = comm_set(dev);
   if (!cs) return 1;
   std::lock_guard<std::mutex> g(cs->mu);
+  t_last_gather = 1;  // this call is RCCL's from here, whatever it returns
+  // On an error after the first launch, wait for the streams that may still
+  // be writing root_out before returning it.
+  int launched = 0;
+  auto fail = [&](int rc) {
+    for (int k = 0; k < launched; k++)
+      if (hipSetDevice(dev[(size_t)k]) == hipSuccess)
+        (void)hipStreamSynchronize(cs->stream[(size_t)k]);
+    return rc;
+  };
   int rc = 0;
   if (nmax > cs->cap) {
+    cs->cap = 0;  // reset first: a failed (re)allocation leaves no stale capacity
     for (int k = 0; k < ns; k++) {
       if ((rc = record_hip(hipSetDevice(dev[(size_t)k])))) return rc;
       if (cs->buf[(size_t)k]) (void)hipFree(cs->buf[(size_t)k]);
@@ -197,6 +231,7 @@ int spans_multi_rccl(const uinet_cksum_shard* shards, int ns, uint32_t flags, ui
     if ((rc = record_hip(hipSetDevice(root_device)))) return rc;
     if (cs->pad) (void)hipFree(cs->pad);
     cs->pad = nullptr;
+    cs->pad_cap = 0;
     if ((rc = record_hip(hipMalloc((void**)&cs->pad, 2 * need)))) return rc;
     cs->pad_cap = need;
   }
@@ -204,40 +239,42 @@ int spans_multi_rccl(const uinet_cksum_shard* shards, int ns, uint32_t flags, ui
   // folds straight into its slice of root_out and gathers in place there
   for (int k = 0; k < ns; k++) {
     const uinet_cksum_shard& sh = shards[k];
-    if ((rc = record_hip(hipSetDevice(sh.device)))) return rc;
+    if ((rc = record_hip(hipSetDevice(sh.device)))) return fail(rc);
     uint16_t* o = (equal && k == root) ? root_out + at[(size_t)k] : cs->buf[(size_t)k];
+    launched = k + 1;
     if (sh.n &&
         (rc = launch_spans(sh.base, sh.off, sh.len, sh.seed, sh.parity, o, sh.n, flags, len_hint,
                            cs->stream[(size_t)k])))
-      return rc;
+      return fail(rc);
   }
   uint16_t* recv = equal ? root_out : cs->pad;
-  if (rccl().group_start() != ncclSuccess) return UINET_CKSUM_EHIP;
+  if (rccl().group_start() != ncclSuccess) return fail(UINET_CKSUM_EHIP);
   for (int k = 0; k < ns; k++) {
     const void* send = (equal && k == root) ? (const void*)(root_out + at[(size_t)k])
                                             : (const void*)cs->buf[(size_t)k];
     if (rccl().gather(send, k == root ? (void*)recv : nullptr, 2 * nmax, ncclUint8, root,
                       cs->comm[(size_t)k], cs->stream[(size_t)k]) != ncclSuccess) {
       (void)rccl().group_end();
-      return UINET_CKSUM_EHIP;
+      return fail(UINET_CKSUM_EHIP);
     }
   }
-  if (rccl().group_end() != ncclSuccess) return UINET_CKSUM_EHIP;
+  if (rccl().group_end() != ncclSuccess) return fail(UINET_CKSUM_EHIP);
   if (!equal) {  // unequal shards: compact the padded slots on the root
-    if ((rc = record_hip(hipSetDevice(root_device)))) return rc;
+    if ((rc = record_hip(hipSetDevice(root_device)))) return fail(rc);
     for (int k = 0; k < ns; k++)
       if (shards[k].n &&
           (rc = record_hip(hipMemcpyAsync(root_out + at[(size_t)k], cs->pad + (uint64_t)k * nmax,
                                           2 * (size_t)shards[k].n, hipMemcpyDeviceToDevice,
                                           cs->stream[(size_t)root]))))
-        return rc;
+        return fail(rc);
   }
+  int first = 0;
   for (int k = 0; k < ns; k++) {
-    if ((rc = record_hip(hipSetDevice(dev[(size_t)k])))) return rc;
-    if ((rc = record_hip(hipStreamSynchronize(cs->stream[(size_t)k])))) return rc;
+    rc = record_hip(hipSetDevice(dev[(size_t)k]));
+    if (!rc) rc = record_hip(hipStreamSynchronize(cs->stream[(size_t)k]));
+    if (rc && !first) first = rc;  // still wait for every other stream
   }
-  t_last_gather = 1;
-  return 0;
+  return first;
 }
 
 int first_error(const std::vector<int>& rc) {
@@ -255,6 +292,7 @@ extern "C" {
 
 int uinet_cksum_spans_multi(const struct uinet_cksum_shard* shards, int nshards, uint32_t flags,
                             uint32_t len_hint, int root_device, uint16_t* root_out) {
+  t_last_gather = -1;  // until a gather runs in this call
   if (nshards < 0 || (nshards > 0 && (!shards || !root_out))) return UINET_CKSUM_EINVAL;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return UINET_CKSUM_ENODEV;

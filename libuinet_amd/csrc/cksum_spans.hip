@@ -110,17 +110,11 @@ __device__ __forceinline__ uint32_t sld_len(const uint16_t* p) {
   return (sld32(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)) >> (8 * (a & 2))) & 0xffffu;
 }
 
-// Four dot2 against (1, 1): both 16-bit halves of every word added into acc.
-__device__ __forceinline__ uint32_t dot_acc(u32x4 v, uint32_t acc) {
-  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-  const us2 one = {1, 1};
-  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, (uint32_t)v.x), one, acc, false);
-  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, (uint32_t)v.y), one, acc, false);
-  acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, (uint32_t)v.z), one, acc, false);
-  return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, (uint32_t)v.w), one, acc, false);
-}
+// Four dot2 against (1, 1): both 16-bit halves of every word added into acc
+// (cksum_device.h: the words are copied out before the bit-cast).
+__device__ __forceinline__ uint32_t dot_acc(u32x4 v, uint32_t acc) { return chunk_halves(v, acc); }
 __device__ __forceinline__ uint32_t dot_acc_masked(u32x4 v, u32x4 m, uint32_t acc) {
-  return dot_acc(v & m, acc);
+  return chunk_halves_masked(v, m, acc);
 }
 
 // x + the value of row_ror:n (lanes rotate by n inside each 16-lane row).
@@ -913,7 +907,7 @@ int launch_spans_quad(const void* base, const OffT* off, const LenT* len,
   const uint32_t remap = (uint32_t)tuning().xcd_remap;
   constexpr bool kWide = sizeof(OffT) == 8;
 #define UINET_QUAD(U, P, SD, ST)                                                             \
-  hipLaunchKernelGGL((k_spans_quad<U, P, SD, ST, OffT, LenT>), grid, blk, 0, stream, b, off, \
+  UINET_LAUNCH((k_spans_quad<U, P, SD, ST, OffT, LenT>), grid, blk, 0, stream, b, off, \
                      len, seed, parity, out, n, flags, remap, stride, slen)
 #define UINET_QUAD_U(U)                                          \
   if (strided) { /* wide descriptors only: none are read */     \
@@ -963,7 +957,7 @@ int launch_spans_lean(const void* base, const OffT* off, const LenT* len,
   const uint32_t remap = (uint32_t)tuning().xcd_remap;
   constexpr bool kWide = sizeof(OffT) == 8;
 #define UINET_LEAN(G, P, SD, ST)                                                              \
-  hipLaunchKernelGGL((k_spans_lean<G, P, SD, ST, OffT, LenT>), grid, blk, 0, stream, b, off, \
+  UINET_LAUNCH((k_spans_lean<G, P, SD, ST, OffT, LenT>), grid, blk, 0, stream, b, off, \
                      len, seed, parity, out, n, flags, remap, stride, slen)
 #define UINET_LEAN_G(G)                                          \
   if (strided) { /* wide descriptors only: none are read */     \
@@ -1003,10 +997,10 @@ int launch_strided_dense(const void* base, uint64_t stride, uint32_t len, const 
   blocks = std::max<uint64_t>(1, std::min(blocks, cap));
   const uint8_t* b = static_cast<const uint8_t*>(base);
   if (seed)
-    hipLaunchKernelGGL((k_strided_dense<true>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream,
+    UINET_LAUNCH((k_strided_dense<true>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream,
                        b, seed, out, n, flags, s, len, kpk, recip);
   else
-    hipLaunchKernelGGL((k_strided_dense<false>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream,
+    UINET_LAUNCH((k_strided_dense<false>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream,
                        b, seed, out, n, flags, s, len, kpk, recip);
   return check_launch();
 }

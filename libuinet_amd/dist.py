@@ -119,3 +119,92 @@ class ResultGather:
             return None
         out = torch.cat([g[: 2 * c] for g, c in zip(self.recv[slot], self.counts)])
         return out.view(dtype or torch.int16)
+
+
+class Watchdog:
+    """Bounded time for every phase of a multi-process run.
+
+    A daemon thread watches the phase this rank is in.  When a phase outlives
+    its deadline (a rendezvous that never completes, an RCCL init or a gather
+    stuck on a peer), the rank prints ONE JSON diagnostic line -- phase, rank,
+    seconds in the phase and since start -- and leaves with ``os._exit`` (no
+    cleanup that could block on the stuck collective, no re-exec, no retry).
+    ``fail(exc)`` does the same for an exception raised inside a phase, so every
+    rank of a broken run ends non-zero with a line that says where.
+
+    Deadlines (seconds) default to :data:`DEFAULTS`; the environment variable
+    ``UINET_BENCH_WATCHDOG_S`` sets one value for every phase.  For tests,
+    ``UINET_BENCH_STALL="<rank>:<phase>"`` makes that rank hang on entering
+    that phase (the watchdog must end it).  The reference's concurrency this
+    guards is one RX/TX kthread per interface
+    (/root/reference/lib/libuinet/uinet_if_netmap.c:1648-1665): one stuck
+    worker must not hang the others silently."""
+
+    DEFAULTS = {"rendezvous": 300.0, "workload": 600.0, "warmup": 300.0, "timed": 300.0,
+                "parity": 900.0, "plan": 120.0, "teardown": 120.0}
+    EXIT_DEADLINE = 124  # timeout(1)'s status
+    EXIT_ERROR = 125
+
+    def __init__(self, rank: int, deadlines=None, stream=None):
+        import os
+        import sys
+        import threading
+        import time
+
+        self._os, self._time = os, time
+        self.rank = int(rank)
+        self.stream = stream or sys.stdout
+        self.deadlines = dict(self.DEFAULTS, **(deadlines or {}))
+        flat = os.environ.get("UINET_BENCH_WATCHDOG_S")
+        if flat:
+            self.deadlines = {k: float(flat) for k in self.deadlines}
+        self.t0 = time.monotonic()
+        self.phase, self.t_phase, self.deadline = None, self.t0, None
+        self._lock = threading.Lock()
+        self._thread = threading.Thread(target=self._watch, name="uinet-watchdog", daemon=True)
+        self._thread.start()
+
+    def enter(self, phase: str) -> None:
+        now = self._time.monotonic()
+        with self._lock:
+            self.phase, self.t_phase = phase, now
+            self.deadline = now + self.deadlines.get(phase, max(self.deadlines.values()))
+        if self._os.environ.get("UINET_BENCH_STALL") == f"{self.rank}:{phase}":
+            while True:  # injected hang (tests): only the watchdog ends it
+                self._time.sleep(3600)
+
+    def done(self) -> None:
+        with self._lock:
+            self.phase, self.deadline = None, None
+
+    def _line(self, what: str, **extra) -> None:
+        import json
+
+        now = self._time.monotonic()
+        rec = {"watchdog": what, "phase": self.phase, "rank": self.rank,
+               "phase_s": round(now - self.t_phase, 3), "elapsed_s": round(now - self.t0, 3),
+               "deadline_s": self.deadlines.get(self.phase) if self.phase else None}
+        rec.update(extra)
+        try:
+            self.stream.write(json.dumps(rec) + "\n")
+            self.stream.flush()
+        except Exception:  # pragma: no cover - nothing left to report with
+            pass
+
+    def fail(self, exc: BaseException) -> None:
+        """Report an exception raised inside the current phase and exit."""
+        self._line("error", error=f"{type(exc).__name__}: {exc}"[:500])
+        self._os._exit(self.EXIT_ERROR)
+
+    def _watch(self) -> None:
+        while True:
+            with self._lock:
+                dl = self.deadline
+            now = self._time.monotonic()
+            if dl is not None and now >= dl:
+                with self._lock:
+                    if self.deadline is None or self._time.monotonic() < self.deadline:
+                        continue
+                    self._line("deadline")
+                self._os._exit(self.EXIT_DEADLINE)
+            self._time.sleep(0.2 if dl is None else min(0.2, max(0.01, dl - now)))

@@ -35,6 +35,8 @@ def exported_functions() -> set[str]:
 
 def test_library_loads():
     assert u.lib().uinet_cksum_version().startswith(b"libuinet_cksum")
+    if not gpu_available():
+        assert u.last_kernel() == ""  # nothing launched on this thread
 
 
 def test_exports_match_header():

@@ -48,3 +48,64 @@ def test_single_gpu_default_is_config2_without_launcher():
     (p,) = _plans(r.stdout)
     assert p == {"rank": 0, "local_rank": 0, "world": 1, "config": "2",
                  "packets_per_gpu": 1048576, "backend": None}
+
+
+def _rank_procs(n, env_extra, args=("--dry-run",)):
+    """n ranks of bench.py started directly (the launcher's env contract:
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), so each rank's own exit status
+    and output are seen, not a launcher's."""
+    port = str(__import__("bench").free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port}, **env_extra)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"),
+                                       "--gpus", str(n), *args], env=env, cwd="/tmp",
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    return procs
+
+
+def _watchdog_lines(stdout):
+    return [json.loads(m) for m in re.findall(r"\{[^{}]*\"watchdog\"[^{}]*\}", stdout)]
+
+
+def test_watchdog_ends_every_rank_of_a_stalled_run():
+    """Rank 1 hangs on entering the plan phase (injected); rank 0 waits for it
+    in the plan barrier.  Both must end non-zero within the deadline, each
+    with one JSON line naming its phase and rank."""
+    import time
+
+    deadline = 6.0
+    t0 = time.monotonic()
+    procs = _rank_procs(2, {"UINET_BENCH_WATCHDOG_S": str(deadline), "UINET_BENCH_STALL": "1:plan"})
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=120)
+        except subprocess.TimeoutExpired:  # pragma: no cover - the failure under test
+            for q in procs:
+                q.kill()
+            raise AssertionError("a rank outlived its watchdog")
+        outs.append((p.returncode, o, e))
+    took = time.monotonic() - t0
+    for r, (rc, o, e) in enumerate(outs):
+        assert rc != 0, (r, o, e[-2000:])
+        lines = _watchdog_lines(o)
+        assert len(lines) == 1, (r, o, e[-2000:])
+        assert lines[0]["rank"] == r and lines[0]["phase"] == "plan", lines
+        assert lines[0]["watchdog"] in ("deadline", "error"), lines
+    stalled = _watchdog_lines(outs[1][1])[0]
+    assert stalled["watchdog"] == "deadline" and outs[1][0] == 124
+    assert stalled["phase_s"] >= deadline
+    # the deadline bounds the run (plus interpreter and torch start-up)
+    assert took < 90, took
+
+
+def test_watchdog_quiet_on_a_healthy_run():
+    procs = _rank_procs(2, {"UINET_BENCH_WATCHDOG_S": "60"})
+    for p in procs:
+        o, e = p.communicate(timeout=120)
+        assert p.returncode == 0, e[-2000:]
+        assert not _watchdog_lines(o)
+        assert len(_plans(o)) == 1

@@ -82,9 +82,17 @@ def main():
         if os.path.exists(a.out):
             with open(a.out) as fh:
                 cur = json.load(fh)
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bench import kernel_src_sha
+
         for k, e in res.items():
             if "hbm_read_bytes_per_launch" in e:
-                cur[a.key] = dict(e, kernel=k, source=os.path.relpath(a.prof_dir))
+                # src_sha: the kernel's sources at measurement time (bench.py
+                # reports the traffic only while they are unchanged)
+                cur[a.key] = dict(e, kernel=k, source=os.path.relpath(a.prof_dir),
+                                  src_sha=kernel_src_sha(k))
         with open(a.out, "w") as fh:
             json.dump(cur, fh, indent=1, sort_keys=True)
 
