@@ -157,14 +157,18 @@ bool ip6_zone_embedded(const uint8_t* a) {
 // the stack walks them: hop-by-hop only first (ip6_input.c:906-913), then the
 // next-header loop (:986-1019) through destination options (dest6.c:62-123)
 // and routing headers (route6.c:59-108: segments left 0 is skipped, anything
-// else dropped on receive); at most 15 headers (ip6_hdrnestlimit).  A
+// else dropped on receive).  The loop counts every header it handles, the
+// transport included, against ip6_hdrnestlimit = 15 (:986-990,
+// in6_proto.c:406); hop-by-hop is handled before the loop and does not count,
+// so a packet may carry hop-by-hop + 14 more headers + the transport.  A
 // fragment header (frag6.c:165) stops the walk: the stack reassembles first.
 // Returns 1 with *off (the transport header's offset from the IPv6 header)
 // and *nxt at the first other header, 0 at a fragment header, -1 when the
 // stack would drop the packet or the walk leaves the payload (ip6_plen).
 int ip6_walk(const MbufHdr* m, const Ip6& ip, bool rx, int* off, int* nxt) {
   int o = 40, x = ip.nxt;
-  for (int k = 0; k < 15; k++) {
+  const int lim = x == 0 ? 16 : 15;  // + the uncounted hop-by-hop header
+  for (int k = 0; k < lim; k++) {
     if (x == 0 && k != 0) return -1;  // hop-by-hop after the first header
     if (x != 0 && x != 43 && x != 60) {
       if (o > 40 + ip.plen) return -1;

@@ -260,8 +260,9 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
     for (int g = 0; g < kP; ++g) {
       const uint32_t qg = s0.q0 + (uint32_t)g;
       const uint32_t lp =
-          kParity ? (s0.lp[g] >> (8 * ((uint32_t)reinterpret_cast<uintptr_t>(parity) + qg))) & 1u
-                  : 0u;
+          kParity
+              ? (s0.lp[g] >> (8u * (((uint32_t)reinterpret_cast<uintptr_t>(parity) + qg) & 3u))) & 1u
+              : 0u;
       b[g] = (lp ^ boff ^ (uint32_t)s0.o[g]) & 1u;
       z.sd[g] = kSeed && qg < n ? fold16_32(s0.sd[g]) : 0u;
     }

@@ -188,16 +188,20 @@ zone_embedded(const uint8_t *a)
  * header, payload length plen): hop-by-hop (0) only as the first header,
  * destination options (60) and routing (43) headers are (len + 1) * 8 bytes,
  * a routing header with segments left is dropped on receive, at most 15
- * headers.  Returns 1 and the transport's offset / protocol, 0 at a fragment
+ * headers after hop-by-hop (the transport included).  Returns 1 and the transport's offset / protocol, 0 at a fragment
  * header (44), -1 for a dropped packet.
  */
 static int
 walk6(const struct oracle_mbuf *ipm, int plen, int first, int rx, int *off, int *nxt)
 {
 	int o = 40, x = first, k;
+	/* ip6_input.c:986-990 counts the loop's headers (transport included)
+	 * against ip6_hdrnestlimit (15, in6_proto.c:406); hop-by-hop (:906-913)
+	 * runs before the loop and does not count */
+	int lim = x == 0 ? 16 : 15;
 	uint8_t e[4];
 
-	for (k = 0; k < 15; k++) {
+	for (k = 0; k < lim; k++) {
 		if (x == 0 && k > 0)
 			return -1;
 		if (x == 44) {

@@ -146,7 +146,7 @@ def _walk6(b: bytes, rx: bool):
     offset) at a fragment header, or None for a packet the stack drops."""
     plen = b[4] << 8 | b[5]
     o, x = 40, b[6]
-    for k in range(15):
+    for k in range(16 if x == 0 else 15):  # hop-by-hop is outside the nest count
         if x == 0 and k > 0:
             return None
         if x not in (0, 43, 60):
@@ -360,4 +360,71 @@ def test_pcap_rx_offload_gpu(torch_dev, ora, pcap_frames):
     rx_o, _ = _pcap_rx(pcap_frames)
     np.testing.assert_array_equal(u.rx_offload(rx_g.heads), ora.rx_offload(rx_o.heads))
     for x, y in zip(pkthdr_fields(rx_g), pkthdr_fields(rx_o)):
+        np.testing.assert_array_equal(x, y)
+
+
+# ---- IPv6 header-nest limit (ip6_input.c:906-913,986-990; in6_proto.c:406) -------
+
+def _nest_frames(cases):
+    """Ethernet + IPv6 + the given extension headers (hop-by-hop first when
+    `hbh`, then `ndst` destination-options headers of 8 bytes) + a TCP header
+    with a correct th_sum + 32 payload bytes, one cluster per frame."""
+    from libuinet_amd.frames import pseudo6
+    from libuinet_amd.mbuf import MbufChains, aligned_empty
+
+    rng = np.random.default_rng(77)
+    frames = []
+    for hbh, ndst in cases:
+        types = ([0] if hbh else []) + [60] * ndst
+        ext = bytearray()
+        for j, _t in enumerate(types):
+            nxt = types[j + 1] if j + 1 < len(types) else 6
+            ext += bytes([nxt, 0, 1, 4, 0, 0, 0, 0])  # PadN over the option space
+        tcp = bytearray(rng.integers(0, 256, 20 + 32, dtype=np.uint8).tobytes())
+        tcp[12] = 5 << 4  # data offset 5
+        tcp[16:18] = b"\0\0"
+        src = bytes([0x20, 0x01]) + rng.integers(0, 256, 14, dtype=np.uint8).tobytes()
+        dst = bytes([0x20, 0x01]) + rng.integers(0, 256, 14, dtype=np.uint8).tobytes()
+        s = pseudo6(src, dst, len(tcp), 6) + int(np.frombuffer(bytes(tcp), "<u2").sum())
+        while s >> 16:
+            s = (s & 0xFFFF) + (s >> 16)
+        tcp[16:18] = (~s & 0xFFFF).to_bytes(2, "little")
+        plen = len(ext) + len(tcp)
+        ip6 = bytes([0x60, 0, 0, 0]) + plen.to_bytes(2, "big") + bytes(
+            [types[0] if types else 6, 64]) + src + dst
+        eth = rng.integers(0, 256, 12, dtype=np.uint8).tobytes() + b"\x86\xdd"
+        frames.append(eth + ip6 + bytes(ext) + bytes(tcp))
+    arena = aligned_empty(2048 * len(frames) + 64)
+    for i, f in enumerate(frames):
+        arena[2048 * i:2048 * i + len(f)] = np.frombuffer(f, np.uint8)
+    ch = MbufChains.contiguous(arena, 2048 * np.arange(len(frames)), [len(f) for f in frames])
+    return ch, frames
+
+
+NEST_CASES = [(True, 13), (True, 14), (True, 15), (False, 13), (False, 14), (False, 15),
+              (True, 0), (False, 0)]
+# the stack reaches tcp6_input (and so reads an offload mark) when the loop's
+# headers, transport included, are at most 15: hop-by-hop + 14, or 14 alone
+NEST_OK = [True, True, False, True, True, False, True, True]
+
+
+def test_ipv6_nest_limit_oracle(ora):
+    ch, frames = _nest_frames(NEST_CASES)
+    for f, ok in zip(frames, NEST_OK):
+        w = _walk6(f[14:], True)
+        assert (w is not None) == ok and (not ok or w[1] == 6)
+    st = ora.rx_offload(ch.heads)
+    assert ((st & RX_IPV6) != 0).all()
+    for s, ok in zip(st, NEST_OK):
+        assert ((s & (RX_L4 | RX_L4_OK)) == (RX_L4 | RX_L4_OK)) == ok, (hex(s), ok)
+
+
+@pytest.mark.gpu
+def test_ipv6_nest_limit_gpu(torch_dev, ora):
+    import libuinet_amd as u
+
+    ch_g, _ = _nest_frames(NEST_CASES)
+    ch_o, _ = _nest_frames(NEST_CASES)
+    np.testing.assert_array_equal(u.rx_offload(ch_g.heads), ora.rx_offload(ch_o.heads))
+    for x, y in zip(pkthdr_fields(ch_g), pkthdr_fields(ch_o)):
         np.testing.assert_array_equal(x, y)
