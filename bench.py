@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=200,
                     help="untimed steps first: the first ~30-100 back-to-back launches run "
-                    "up to 25 %% slower while clocks settle (tools/drift.py)")
+                    "up to 25 %% slower while clocks settle (profiles/r01/)")
     ap.add_argument("--config", choices=["2", "2rx", "2s", "2su", "3", "3tx", "4", "5", "5tso"],
                     default=None,
                     help="BASELINE.json config shape (default: 2 = the headline at N = 1, 4 = "

@@ -150,13 +150,14 @@ int uinet_cksum_device_ok(void);
  *   "chains_long"     chain segments of at least this many 16-B chunks are
  *                     streamed wave-wide; 0 = never, else >= 16 (default 128)
  *   "chains_tile"     packets per wave in the chain kernel: 0 = auto, 8, 32
+ *   "chains_sweep"    chain kernel: descriptor rounds whose segments lie in
+ *                     one dense address range are read as plain chunks with
+ *                     a running prefix, windows of 2 (default) or 4 x 64
+ *                     chunks; 0 = every round through the chunk list
  *   "xcd_remap"       span kernels: give each XCD a contiguous band of
  *                     packets (1, default) or plain block order (0)
  *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
  *                     1..64 (default min(16, hardware threads))
- *   "spans_sdesc"     one-shot span kernel (spans_pipe 0) with 32 or 64 lanes
- *                     per packet: the wave's packet descriptors by scalar
- *                     loads (1, default) or one vector load per lane group (0)
  *   "spans_pipe"      span kernel family (span and strided APIs):
  *                     1 (default) persistent waves with mask-free whole
  *                     chunks and the per-packet work shared across the wave
@@ -166,10 +167,7 @@ int uinet_cksum_device_ok(void);
  *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
  *                     16x3, 32x3, 64x2, 64x3); 0 = picked from len_hint
  *   "walk_prefetch"   host-mbuf batch walk: 0 = no prefetch, 1 = prefetch
- *                     mbuf headers a few packets ahead (default), 2 = chase
- *                     16 chains in lockstep (never changes results)
- *   "host_group"      zero-copy host-mbuf batches: chunks per host thread in
- *                     one pipeline group (1..64, default 1)
+ *                     mbuf headers a few packets ahead (default)
  *   "host_pin"        host pool helpers pinned to CPUs of the process mask
  *                     (1) or floating (0, default)
  *   "multi_gather"    uinet_cksum_spans_multi: 0 = one RCCL gather when it
@@ -178,9 +176,9 @@ int uinet_cksum_device_ok(void);
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU,
  * UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG, UINET_CKSUM_CHAINS_TILE,
  * UINET_CKSUM_XCD_REMAP, UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF,
- * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_SDESC, UINET_CKSUM_SPANS_PIPE,
- * UINET_CKSUM_HOST_GROUP, UINET_CKSUM_HOST_PIN and UINET_CKSUM_MULTI_GATHER
- * set the initial values. */
+ * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_PIPE, UINET_CKSUM_HOST_PIN,
+ * UINET_CKSUM_MULTI_GATHER and UINET_CKSUM_CHAINS_SWEEP set the initial
+ * values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
 /* ------------------------------------------------------------------------ */

@@ -63,8 +63,8 @@ void note_kernel(const void* host_stub) { t_last_kernel = host_stub; }
 // (tuning()).  The environment seeds them through the same validation.
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_pass{2}, host_threads{8}, chains_long{128},
-      chains_tile{0}, xcd_remap{1}, walk_prefetch{1}, spans_geo{0}, spans_sdesc{1},
-      spans_pipe{1}, host_group{1}, host_pin{0}, multi_gather{0}, chains_sweep{2};
+      chains_tile{0}, xcd_remap{1}, walk_prefetch{1}, spans_geo{0}, spans_pipe{1},
+      host_pin{0}, multi_gather{0}, chains_sweep{2};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -83,10 +83,8 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"xcd_remap", &TuningLive::xcd_remap, [](int v) { return v == 0 || v == 1; }},
       {"host_threads", &TuningLive::host_threads, [](int v) { return v >= 1 && v <= 64; }},
       {"spans_geo", &TuningLive::spans_geo, [](int v) { return v == 0 || span_geometry_ok(v); }},
-      {"spans_sdesc", &TuningLive::spans_sdesc, [](int v) { return v == 0 || v == 1; }},
       {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v == 0 || v == 1; }},
-      {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v >= 0 && v <= 2; }},
-      {"host_group", &TuningLive::host_group, [](int v) { return v >= 1 && v <= 64; }},
+      {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v == 0 || v == 1; }},
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
       {"chains_sweep", &TuningLive::chains_sweep, [](int v) { return v == 0 || v == 2 || v == 4; }},
@@ -106,8 +104,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_CHAINS_LONG", "chains_long"},     {"UINET_CKSUM_CHAINS_TILE", "chains_tile"},
         {"UINET_CKSUM_XCD_REMAP", "xcd_remap"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
         {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_GEO", "spans_geo"},
-        {"UINET_CKSUM_SPANS_SDESC", "spans_sdesc"},
-        {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},       {"UINET_CKSUM_HOST_GROUP", "host_group"},
+        {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},
         {"UINET_CKSUM_HOST_PIN", "host_pin"},          {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},
         {"UINET_CKSUM_CHAINS_SWEEP", "chains_sweep"},
     };
@@ -115,7 +112,7 @@ static TuningLive& tuning_live() {
       const char* e = getenv(kv[0]);
       if (!e || !*e) continue;
       int v = atoi(e);
-      if (!strcmp(kv[1], "xcd_remap") || !strcmp(kv[1], "spans_sdesc"))
+      if (!strcmp(kv[1], "xcd_remap"))
         v = v ? 1 : 0;
       if (std::atomic<int>* f = tuning_field(*x, kv[1], v)) f->store(v, std::memory_order_relaxed);
     }
@@ -136,9 +133,7 @@ Tuning tuning() {
   x.xcd_remap = ld(t.xcd_remap);
   x.walk_prefetch = ld(t.walk_prefetch);
   x.spans_geo = ld(t.spans_geo);
-  x.spans_sdesc = ld(t.spans_sdesc);
   x.spans_pipe = ld(t.spans_pipe);
-  x.host_group = ld(t.host_group);
   x.host_pin = ld(t.host_pin);
   x.multi_gather = ld(t.multi_gather);
   x.chains_sweep = ld(t.chains_sweep);
@@ -253,6 +248,7 @@ struct PacketWalk {
   long remain = 0;  // bytes still wanted
   long first_clen = 0;
   bool have_first = false;
+  bool long_piece = false;  // a piece over 65535 B since the owner last cleared it
 
   void reset(long want) {
     bytes = 0;
@@ -274,6 +270,7 @@ struct PacketWalk {
         first_clen = clen;
       }
       out->push_back({addr, (uint32_t)mlen});
+      long_piece |= mlen > 0xffff;
       bytes += (uint64_t)mlen;
     }
     clen += mlen;
@@ -376,6 +373,7 @@ struct Chunk {
   uint32_t first_piece = 0;    // global index of pieces[0]
   uint64_t pack_base = 0;      // staging offset of packet i0
   bool odd = false, too_big = false, unmapped = false;
+  bool long_piece = false;     // a piece over 65535 B: its group takes wide descriptors
 };
 
 // Per-thread scratch, reused across calls.
@@ -428,8 +426,21 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   double t_walk = 0, t_desc = 0;
   int rc = ctx_reserve(c, std::max<size_t>(c.h_cap, 1u << 20), (size_t)n, false);
   if (rc) return rc;
-  uint64_t lo_addr = ~0ull;
-  for (const Region& r : g_regions) lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
+  uint64_t lo_addr = ~0ull, hi_addr = 0;
+  for (const Region& r : g_regions) {
+    lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
+    hi_addr = std::max(hi_addr, (uint64_t)(r.end + r.delta));
+  }
+  // Packed 6-B descriptors (u32 offset, u16 length: launch_chains32) when every
+  // registered byte lies within 4 GiB of the lowest and no piece is longer than
+  // 65535 B, else the 12-B wide ones.  The kernel reads them over PCIe, where a
+  // byte costs ~140x what it does in HBM.  A group holding a longer piece is
+  // written wide (its chunks flag it).
+#ifdef UINET_HOST_WIDE_DESC  // lab A/B build only (tools/r04_hostdesc.sh)
+  const bool span32 = false;
+#else
+  const bool span32 = hi_addr - lo_addr <= 0x100000000ull;
+#endif
   void* dout = nullptr;
   rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
   if (rc) return rc;
@@ -439,8 +450,9 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   const std::vector<Region>& regs = g_regions;
   const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const auto drain = [&]() { return record_hip(hipStreamSynchronize(c.stream)); };
-  // chunks per pipeline group: host_group per thread (one pool pass each)
-  const int group = std::max(1, threads) * std::max(1, tuning().host_group);
+  // chunks per pipeline group: one per thread (one pool pass each; 2-64 per
+  // thread lost in every A/B, profiles/r04/pruned/knobs.diff)
+  const int group = std::max(1, threads);
   const bool pin = tuning().host_pin != 0;
   size_t ring = 0;  // next free byte of the descriptor ring in c.h_buf
   uint64_t total = 0;
@@ -469,7 +481,9 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
     const size_t np = (size_t)np64;
     const int i0 = B.chunks[(size_t)g0].i0;
     const int ng = B.chunks[(size_t)g1 - 1].i1 - i0;
-    const size_t o_len = a16(8 * np), o_ps = o_len + a16(4 * np);
+    bool packed = span32;
+    for (int j = g0; j < g1 && packed; j++) packed = !B.chunks[(size_t)j].long_piece;
+    const size_t o_len = a16((packed ? 4 : 8) * np), o_ps = o_len + a16((packed ? 2 : 4) * np);
     const size_t o_sd = o_ps + a16(4 * ((size_t)ng + 1)), need = o_sd + a16(4 * (size_t)ng);
     if (ring + need > c.h_cap) {
       // the ring is full: wait for the launched groups, then reuse it from
@@ -487,6 +501,8 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
     uint8_t* h = c.h_buf + ring;
     uint64_t* so = reinterpret_cast<uint64_t*>(h);
     uint32_t* sl = reinterpret_cast<uint32_t*>(h + o_len);
+    uint32_t* so32 = reinterpret_cast<uint32_t*>(h);
+    uint16_t* sl16 = reinterpret_cast<uint16_t*>(h + o_len);
     uint32_t* ps = reinterpret_cast<uint32_t*>(h + o_ps);
     uint32_t* sd = reinterpret_cast<uint32_t*>(h + o_sd);
     pool.run(g1 - g0, threads, [&](int jj) {
@@ -499,8 +515,13 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
           C.unmapped = true;
           return;
         }
-        so[k0 + k] = dev - lo_addr;
-        sl[k0 + k] = C.pieces[k].n;
+        if (packed) {
+          so32[k0 + k] = (uint32_t)(dev - lo_addr);
+          sl16[k0 + k] = (uint16_t)C.pieces[k].n;
+        } else {
+          so[k0 + k] = dev - lo_addr;
+          sl[k0 + k] = C.pieces[k].n;
+        }
       }
       for (int i = C.i0; i < C.i1; i++) {
         ps[i - i0] = C.first_piece + B.pk_first[(size_t)i];
@@ -515,13 +536,22 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
       return rc ? rc : kFallback;
     }
     uint8_t* d = static_cast<uint8_t*>(dbuf) + ring;
-    rc = launch_chains(reinterpret_cast<const void*>(lo_addr),
-                       reinterpret_cast<const uint64_t*>(d),
-                       reinterpret_cast<const uint32_t*>(d + o_len),
-                       reinterpret_cast<const uint32_t*>(d + o_ps), nullptr, nullptr,
-                       reinterpret_cast<const uint32_t*>(d + o_sd),
-                       static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags,
-                       np ? (uint32_t)(tot_g / np) : 1u, c.stream);
+    if (packed)
+      rc = launch_chains32(reinterpret_cast<const void*>(lo_addr),
+                           reinterpret_cast<const uint32_t*>(d),
+                           reinterpret_cast<const uint16_t*>(d + o_len),
+                           reinterpret_cast<const uint32_t*>(d + o_ps), nullptr, nullptr,
+                           reinterpret_cast<const uint32_t*>(d + o_sd),
+                           static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags,
+                           np ? (uint32_t)(tot_g / np) : 1u, c.stream);
+    else
+      rc = launch_chains(reinterpret_cast<const void*>(lo_addr),
+                         reinterpret_cast<const uint64_t*>(d),
+                         reinterpret_cast<const uint32_t*>(d + o_len),
+                         reinterpret_cast<const uint32_t*>(d + o_ps), nullptr, nullptr,
+                         reinterpret_cast<const uint32_t*>(d + o_sd),
+                         static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags,
+                         np ? (uint32_t)(tot_g / np) : 1u, c.stream);
     if (rc) {
       (void)drain();
       return rc;
@@ -548,21 +578,13 @@ struct ChainRef {
   long limit;        // bytes from the chain start the walk consumes
 };
 
-// Walk prefetch.  The walk is bound by
-// misses on mbuf headers (m_next/m_data/m_len share the first line), each
-// dependent on the previous one, so walking one chain after another keeps
-// about one miss in flight per thread.  The default (prefetch_ahead) requests
-// headers a few packets ahead.  The alternative (=2, kept for A/B; equal on
-// config 3, 3-12 % slower on the offload hooks in profiles/r01/ab/walk_pf/):
-// before packets [i, i + kChase) are
-// walked, the chains of [i + kChase, i + 2 kChase) are chased side by side,
-// one mbuf of each per step: kChase independent misses in flight, and the
-// walk then finds its headers in cache.  A chase reads m_len/m_next only of
-// mbufs the walk itself reads: it stops once a chain's lengths reach the
-// bytes the packet wants from the chain start (`ChainRef::limit`).
-// Tuning knob "walk_prefetch" (env UINET_CKSUM_WALK_PF): 0 off, 1 ahead, 2 chase.
-constexpr int kChase = 16;
-
+// Walk prefetch.  The walk is bound by misses on mbuf headers
+// (m_next/m_data/m_len share the first line), each dependent on the previous
+// one, so walking one chain after another keeps about one miss in flight per
+// thread.  prefetch_ahead requests headers a few packets ahead (knob
+// "walk_prefetch", env UINET_CKSUM_WALK_PF: 1 default, 0 off).  A lockstep
+// chase of 16 chains (equal on config 3, 3-12 % slower on the offload hooks,
+// profiles/r01/ab/walk_pf/) was removed in round 4 (profiles/r04/pruned/).
 // Plain software prefetch ahead: packet i+16's head, i+8's second mbuf,
 // i+4's third (each read from a line an earlier step requested).
 inline void prefetch_ahead(const ChainRef& r, int depth) {
@@ -573,25 +595,6 @@ inline void prefetch_ahead(const ChainRef& r, int depth) {
     h = rem > 0 ? h->m_next : nullptr;
   }
   if (h) __builtin_prefetch(h, 0, 3);
-}
-
-inline void chase_chains(const ChainRef* r, int k) {
-  const MbufHdr* h[kChase];
-  long rem[kChase];
-  for (int j = 0; j < k; j++) {
-    h[j] = r[j].limit > 0 ? r[j].m : nullptr;
-    rem[j] = r[j].limit;
-  }
-  for (bool any = true; any;) {
-    any = false;
-    for (int j = 0; j < k; j++) {
-      const MbufHdr* m = h[j];
-      if (!m) continue;
-      rem[j] -= m->m_len;
-      h[j] = rem[j] > 0 ? m->m_next : nullptr;
-      any |= h[j] != nullptr;
-    }
-  }
 }
 
 // Walk every packet (`walk(i, pw)` fills pw and returns the packet's seed;
@@ -627,7 +630,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   using clk = std::chrono::steady_clock;
   const clk::time_point t_start = trace ? clk::now() : clk::time_point();
   clk::time_point t_walk, t_place, t_fill, t_launch;
-  const int prefetch = tuning().walk_prefetch;  // 0 off, 1 ahead (default), 2 chase
+  const int prefetch = tuning().walk_prefetch;  // 0 off, 1 ahead (default)
 
   // Walk chunk j: every packet as the reference walks it, into the chunk's
   // piece list (pk_first chunk-local).
@@ -639,15 +642,8 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     C.w.out = &C.pieces;
     C.total = C.packed = 0;
     C.odd = C.too_big = C.unmapped = false;
-    ChainRef refs[kChase];
-    const auto chase = [&](int a) {
-      const int k = std::min(kChase, C.i1 - a);
-      for (int j = 0; j < k; j++) refs[j] = head(a + j);
-      if (k > 0) chase_chains(refs, k);
-    };
-    if (prefetch == 2) chase(C.i0);
+    C.w.long_piece = false;
     for (int i = C.i0; i < C.i1; i++) {
-      if (prefetch == 2 && (i - C.i0) % kChase == 0) chase(i + kChase);
       if (prefetch == 1) {
         if (i + 16 < C.i1) prefetch_ahead(head(i + 16), 0);
         if (i + 8 < C.i1) prefetch_ahead(head(i + 8), 1);
@@ -663,10 +659,11 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
       C.total += nb;
       C.packed += (nb + 15) & ~uint64_t(15);
     }
+    C.long_piece = C.w.long_piece;
   };
 
   // (Z) Registered memory: zero-copy, pipelined.  Groups of `threads` chunks
-  // are walked, described (12-B chain descriptors in pinned memory, packet
+  // are walked, described (6-B or 12-B chain descriptors in pinned memory, packet
   // bytes read in place over PCIe) and launched one after another, so the
   // host walks group g+1 while the GPU folds group g.  A group whose pieces
   // are not all registered (or that starts at an odd logical parity: the

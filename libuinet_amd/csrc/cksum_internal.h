@@ -20,14 +20,11 @@ struct Tuning {
                        // wave-wide (0 = never)
   int chains_tile;     // flat chains: packets per wave tile, 0 = auto, 8, 32
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
-  int spans_sdesc;     // span kernels: per-wave scalar descriptor loads (0/1)
   int spans_pipe;      // span kernel family: 1 k_spans_lean / k_spans_quad (persistent,
                        // mask-free whole chunks), 0 one-shot k_spans
   int spans_geo;       // span kernels: lanes-per-packet G and loads-per-lane U
                        // as G * 16 + U (0 = picked from the mean length)
-  int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead, 2 lockstep chase
-  int host_group;      // zero-copy host batches: chunks per thread in one pipeline
-                       // group (a pool pass walks a group while the GPU folds the last)
+  int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead
   int host_pin;        // host pool helpers pinned to CPUs 1.. of the process mask (0/1)
   int multi_gather;    // uinet_cksum_spans_multi: 0 RCCL gather when it applies, 1 peer copies
   int chains_sweep;    // chain kernel: address-sweep window in 64-chunk passes (2, 4), 0 = off

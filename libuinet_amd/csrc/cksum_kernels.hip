@@ -253,16 +253,16 @@ static int launch_spans_t(const void* base, const OffT* off, const LenT* len,
   if (n == 0) return UINET_CKSUM_OK;
   const Geometry geo = geometry_override(pick_geometry(len_hint));
   const int pipe = tuning().spans_pipe;
-  // Scalar descriptors (G >= 32, knob "spans_sdesc", default on): a wave's
-  // 1-2 packets' off / len come from s_loads, and the grid drops to one packet
-  // per group (512 blocks per CU at 1 M x 1500 B).  Interleaved A/B, config 2
-  // (profiles/r02/ab_sdesc/): vector descriptors at 256 / CU 0.2192 ms,
-  // scalar at 256 / CU 0.2167, scalar at 512 / CU 0.2086 (+5.1 %), 4096 / CU
-  // 0.2095; on a slower stretch of the same box +1.4 %.
+  // Scalar descriptors for G >= 32: a wave's 1-2 packets' off / len come from
+  // s_loads, and the grid drops to one packet per group (512 blocks per CU at
+  // 1 M x 1500 B).  Interleaved A/B, config 2 (profiles/r02/ab_sdesc/): vector
+  // descriptors at 256 / CU 0.2192 ms, scalar at 256 / CU 0.2167, scalar at
+  // 512 / CU 0.2086 (+5.1 %), 4096 / CU 0.2095.  (The vector-descriptor form
+  // was the knob spans_sdesc = 0 until round 4: profiles/r04/pruned/.)
   if (pipe == 1 && geo.g == 4)
     return launch_spans_quad(base, off, len, seed, parity, out, n, flags, geo.u, false, 0, 0,
                              blocks_per_cu(128), stream);
-  const bool sdesc = tuning().spans_sdesc && geo.g >= 32;
+  const bool sdesc = geo.g >= 32;
   if (sdesc && pipe == 1 && geo.u == 3)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, false, 0, 0,
                              tuning().blocks_per_cu, stream);

@@ -625,7 +625,7 @@ def test_host_batch_chunked(torch_dev, ora, host_threads):
         u.set_tuning("host_threads", 16)
 
 
-@pytest.mark.parametrize("walk_prefetch", [0, 1, 2])
+@pytest.mark.parametrize("walk_prefetch", [0, 1])
 def test_host_walk_prefetch_variants(torch_dev, ora, walk_prefetch):
     """Every host-walk prefetch mode gives the oracle's sums: chains longer
     than the bytes wanted (the prefetch must stop where the walk stops), short
