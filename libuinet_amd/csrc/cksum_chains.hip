@@ -115,7 +115,7 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 // is < 16 KiB, its weighted sum < 2^29).  One u64 LDS atomic per segment puts
 // it into its (packet, parity) bin.  Rounds that do not qualify (segments
 // scattered over more than 1.25x their own chunks) take the chunk list below.
-template <int kPass, int kTile, int kSweep, typename OffT, typename LenT>
+template <int kPass, int kTile, int kSweep, bool kSweepDbl, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
                                                        const LenT* __restrict__ seg_len,
@@ -320,18 +320,19 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
           const uint32_t tb = ((uint32_t)a_end & 15u) + 1u;  // bytes up to the last
           u32x4* swd = lds_swd[wid];
           uint32_t* swf = lds_swf[wid];
-          u32x4 v[kSweep];
-          // chunks past the range read 0 (buffer range check): no clamp, no fault
-          auto sweep_load = [&](uint32_t w0) {
+          uint32_t seg = 0;    // F(end) - F(start), modulo 2^32
+          uint32_t fbase = 0;  // F at the window's first chunk
+          // chunks past the range read 0 (buffer range check): no clamp, no
+          // fault, no memory traffic -- so loads are issued unconditionally
+          auto sweep_load = [&](u32x4 (&v)[kSweep], uint32_t w0) {
 #pragma unroll
             for (int q = 0; q < kSweep; ++q)
               v[q] = __builtin_amdgcn_raw_buffer_load_b128(
                   sr, (int)(16u * (w0 + (uint32_t)(q * 64 + lane))), 0, 2);
           };
-          uint32_t seg = 0;    // F(end) - F(start), modulo 2^32
-          uint32_t fbase = 0;  // F at the window's first chunk
-          sweep_load(0);
-          for (uint32_t w0 = 0; w0 < span; w0 += (uint32_t)kSwCh) {
+          // one window: chunk sums, the prefix F, staging, then the
+          // segments whose first / last kept byte lies in it
+          auto sweep_window = [&](const u32x4 (&v)[kSweep], uint32_t w0) {
             uint32_t s[kSweep], I[kSweep];
 #pragma unroll
             for (int q = 0; q < kSweep; ++q) {
@@ -346,11 +347,36 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
               fbase += readlane_u32(I[q], 63);
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (w0 + (uint32_t)kSwCh < span) sweep_load(w0 + (uint32_t)kSwCh);
+          };
+          auto sweep_eval = [&](uint32_t w0) {
             const uint32_t js = sc - w0, je = ec - w0;
             if (js < (uint32_t)kSwCh) seg -= chunk_halves_masked(swd[js], lut.m[hb], swf[js]);
             if (je < (uint32_t)kSwCh) seg += chunk_halves_masked(swd[je], lut.m[tb], swf[je]);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          };
+          u32x4 va_[kSweep];
+          sweep_load(va_, 0);
+          if constexpr (!kSweepDbl) {
+            for (uint32_t w0 = 0; w0 < span; w0 += (uint32_t)kSwCh) {
+              sweep_window(va_, w0);
+              // the next window's loads fly while this one's segments are read
+              if (w0 + (uint32_t)kSwCh < span) sweep_load(va_, w0 + (uint32_t)kSwCh);
+              sweep_eval(w0);
+            }
+          } else {
+            // two register sets, two windows in flight: window w + 1 is loading
+            // while window w is summed and scanned (no copy between the sets:
+            // a copy would wait for the load it copies)
+            u32x4 vb_[kSweep];
+            for (uint32_t w0 = 0; w0 < span; w0 += 2u * (uint32_t)kSwCh) {
+              sweep_load(vb_, w0 + (uint32_t)kSwCh);
+              sweep_window(va_, w0);
+              sweep_eval(w0);
+              sweep_load(va_, w0 + 2u * (uint32_t)kSwCh);
+              if (w0 + (uint32_t)kSwCh >= span) break;
+              sweep_window(vb_, w0 + (uint32_t)kSwCh);
+              sweep_eval(w0 + (uint32_t)kSwCh);
+            }
           }
           if (li) atomicAdd(&acc[meta], (unsigned long long)seg);
           continue;
@@ -484,14 +510,17 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
-#define LF(P, T, S)                                                                        \
-  UINET_LAUNCH((k_chains_pipe<P, T, S, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, \
-                     stream, b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
-#define LFS(P, T)                        \
-  do {                                   \
-    if (tn.chains_sweep == 4) LF(P, T, 4); \
-    else if (tn.chains_sweep == 2) LF(P, T, 2); \
-    else LF(P, T, 0);                    \
+#define LF(P, T, S, D)                                                                       \
+  UINET_LAUNCH((k_chains_pipe<P, T, S, D, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0,   \
+               stream, b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
+  // chains_sweep: 0 off; 2 / 4 = windows of 2 / 4 passes; 3 = windows of 2
+  // passes, two in flight
+#define LFS(P, T)                                  \
+  do {                                             \
+    if (tn.chains_sweep == 4) LF(P, T, 4, false);  \
+    else if (tn.chains_sweep == 3) LF(P, T, 2, true); \
+    else if (tn.chains_sweep == 2) LF(P, T, 2, false); \
+    else LF(P, T, 0, false);                       \
   } while (0)
   if (tile == 8) {
     if (tn.chains_pass == 4) LFS(4, 8);
