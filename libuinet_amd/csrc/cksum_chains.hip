@@ -100,7 +100,8 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 #ifdef UINET_CHAINS_WAVES
 #define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(UINET_CHAINS_WAVES)))
 #else
-#define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(kPass == 2 ? 7 : 1)))
+#define UINET_CHAINS_OCC \
+  __attribute__((amdgpu_waves_per_eu(kPass == 2 ? (kSweep == 2 ? 6 : 7) : 1)))
 #endif
 
 // kSweep > 0 adds the address sweep (a descriptor round whose list segments

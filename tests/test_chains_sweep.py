@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import libuinet_amd as u
+from libuinet_amd.mbuf import aligned_empty
 
 from test_gpu_parity import dev, host16, rand_arena, torch_dev  # noqa: F401
 
@@ -131,7 +132,8 @@ def test_sweep_extremes(torch_dev, ora, sweep):
     torch = torch_dev
     rng = np.random.default_rng(14000 + sweep)
     for fill in (0x00, 0xFF):
-        arena = np.full(1 << 20, fill, np.uint8)
+        arena = aligned_empty(1 << 22)
+        arena[:] = fill
         seg_off, seg_len, pkt_seg = dense_layout(rng, 2000, arena.size, "in")
         length, skip, seed = clip_args(rng, seg_len, pkt_seg)
         seed[:] = 0
