@@ -221,34 +221,167 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint64_t so = so_next;
       const uint32_t l = l_next;
       if (r0 + 64 < S1) fetch(r0 + 64);
-      const bool pk_in = lane < np && ps >= r0 && ps < r0 + 64;
-      if (pk_in) atomicMax(&pkmark[ps - r0], (uint32_t)lane + 1);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      const uint32_t pk = pkmark[lane];
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (pk_in) pkmark[ps - r0] = 0;
-      const uint32_t slot1 = max(wave_scan<1, false>(pk, 0u), carry_slot1);
-      const uint32_t slot = slot1 - 1;
-      // chain position: T = carry_pos + exclusive prefix of the lengths never
-      // decreases along the lanes, so the max-scan of T at packet starts is
-      // T at this segment's packet start (0 while the packet of the previous
-      // round continues: its position is T itself)
-      const uint32_t T = carry_pos + wave_scan<0, false>(l, 0u) - l;
-      const uint32_t pos = T - wave_scan<1, false>(pk ? T : 0u, 0u);
-      carry_slot1 = __builtin_amdgcn_readlane(slot1, 63);
-      carry_pos = __builtin_amdgcn_readlane(pos + l, 63);
-      const uint32_t sk = __shfl(k_skip, (int)slot);
-      const uint32_t ln = __shfl(k_len, (int)slot);
-      const uint32_t lo = sk > pos ? min(sk - pos, l) : 0u;
-      const uint32_t hi = ln > pos ? min(ln - pos, l) : 0u;
-      const uint32_t eff = hi > lo ? hi - lo : 0u;
-      const uint64_t ao = so + lo;
-      const uint32_t head = eff ? (uint32_t)(reinterpret_cast<uintptr_t>(base + ao) & 15) : 0u;
-      // chunks touched, without forming head + eff (a u32 segment may be 4 GiB)
-      const uint32_t nch = eff ? (eff >> 4) + ((head + (eff & 15u) + 15u) >> 4) : 0u;
-      const uint64_t c0 = ao - head;
-      const uint32_t rot = ((pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(base + ao)) & 1u;
-      const uint32_t meta = (slot << 1) | rot;
+      // The round's per-segment work: packet slot, chain position, the clip
+      // to [skip, len), chunk count, bin.  It reads the carries of the
+      // previous round and returns the new ones (the caller commits them).
+      struct Desc {
+        uint32_t slot, pos, eff, head, nch, rot, meta, carry_slot1, carry_pos;
+        uint64_t ao, c0;
+      };
+      auto describe = [&]() {
+        Desc D;
+        const bool pk_in = lane < np && ps >= r0 && ps < r0 + 64;
+        if (pk_in) atomicMax(&pkmark[ps - r0], (uint32_t)lane + 1);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint32_t pk = pkmark[lane];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (pk_in) pkmark[ps - r0] = 0;
+        const uint32_t slot1 = max(wave_scan<1, false>(pk, 0u), carry_slot1);
+        D.slot = slot1 - 1;
+        // chain position: T = carry_pos + exclusive prefix of the lengths never
+        // decreases along the lanes, so the max-scan of T at packet starts is
+        // T at this segment's packet start (0 while the packet of the previous
+        // round continues: its position is T itself)
+        const uint32_t T = carry_pos + wave_scan<0, false>(l, 0u) - l;
+        D.pos = T - wave_scan<1, false>(pk ? T : 0u, 0u);
+        D.carry_slot1 = __builtin_amdgcn_readlane(slot1, 63);
+        D.carry_pos = __builtin_amdgcn_readlane(D.pos + l, 63);
+        const uint32_t sk = __shfl(k_skip, (int)D.slot);
+        const uint32_t ln = __shfl(k_len, (int)D.slot);
+        const uint32_t lo = sk > D.pos ? min(sk - D.pos, l) : 0u;
+        const uint32_t hi = ln > D.pos ? min(ln - D.pos, l) : 0u;
+        D.eff = hi > lo ? hi - lo : 0u;
+        D.ao = so + lo;
+        D.head = D.eff ? (uint32_t)(reinterpret_cast<uintptr_t>(base + D.ao) & 15) : 0u;
+        // chunks touched, without forming head + eff (a u32 segment may be 4 GiB)
+        D.nch = D.eff ? (D.eff >> 4) + ((D.head + (D.eff & 15u) + 15u) >> 4) : 0u;
+        D.c0 = D.ao - D.head;
+        D.rot = ((D.pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(base + D.ao)) & 1u;
+        D.meta = (D.slot << 1) | D.rot;
+        return D;
+      };
+      // --- the address sweep -------------------------------------------------
+      // Decided first from the raw descriptors alone (before the clip), so the
+      // range's first windows load while `describe` runs.  The round
+      // qualifies when it holds no long segment and its segments, in lane
+      // order, start at non-decreasing addresses, leave no hole of 4 KiB or
+      // more between them (every byte the sweep reads then shares a 4-KiB page
+      // with a segment byte: nothing unmapped is touched), and fill at least
+      // 4/5 of their range.  Then every list segment's kept bytes [a, a + eff)
+      // must lie in it (they do, clipping only shrinks a segment), else the
+      // round is described again and takes the chunk list.
+      if constexpr (kSweep > 0) {
+        const uint32_t lthr = (long_ch != 0 && long_ch < kListMax) ? long_ch : kListMax;
+        const uint64_t a0 = reinterpret_cast<uintptr_t>(base) + so;
+        const uint32_t rnch = l ? (uint32_t)(((a0 + l - 1) >> 4) - (a0 >> 4)) + 1u : 0u;
+        const bool el = l != 0;
+        const uint64_t em = __ballot(el);
+        bool ok = em != 0 && __ballot(rnch >= lthr) == 0;
+        uint64_t XB = 0;
+        uint32_t span = 0;
+        if (ok) {
+          const int fl = (int)__builtin_ctzll(em);
+          XB = readlane_u64((uint32_t)a0, (uint32_t)(a0 >> 32), fl) & ~15ull;
+          const uint64_t d = a0 - XB;  // huge when below XB: fails the order test
+          const bool near = d < (1ull << 30);
+          const uint32_t rs = el ? (uint32_t)d : 0u;
+          const uint32_t re = el ? rs + l : 0u;
+          const uint32_t ms = wave_scan<1, false>(rs, 0u);  // max start so far
+          const uint32_t me = wave_scan<1, false>(re, 0u);  // max end so far
+          const uint32_t ms_prev = wave_shr1(ms), me_prev = wave_shr1(me);
+          const bool bad =
+              el && (!near || rs < ms_prev || (rs > me_prev && rs - me_prev >= 4096u));
+          const uint32_t C0 = readlane_u32(wave_scan<0, false>(rnch, 0u), 63);
+          span = ((readlane_u32(me, 63) - 1u) >> 4) + 1u;
+          ok = __ballot(bad) == 0 && span <= C0 + (C0 >> 2) + 64u;
+        }
+        if (ok) {
+          const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+              reinterpret_cast<void*>(XB), 0, (int)(16u * span), 0x00020000);
+          // chunks past the range read 0 (buffer range check): no clamp, no
+          // fault, no memory traffic -- so loads are issued unconditionally
+          auto sweep_load = [&](u32x4 (&v)[kSweep], uint32_t w0) {
+#pragma unroll
+            for (int q = 0; q < kSweep; ++q)
+              v[q] = __builtin_amdgcn_raw_buffer_load_b128(
+                  sr, (int)(16u * (w0 + (uint32_t)(q * 64 + lane))), 0, 2);
+          };
+          u32x4 va[kSweep], vb[kSweepDbl ? kSweep : 1];
+          sweep_load(va, 0);
+          if constexpr (kSweepDbl) sweep_load(vb, (uint32_t)kSwCh);
+          const Desc D = describe();
+          const bool li = D.nch != 0;
+          const uint64_t a_abs = reinterpret_cast<uintptr_t>(base) + D.ao;  // first kept byte
+          const uint64_t a_end = a_abs + D.eff - 1;                         // last kept byte
+          const bool in = !li || (a_abs - XB < 16ull * span && a_end - XB < 16ull * span);
+          if (__ballot(!in) == 0) {
+            carry_slot1 = D.carry_slot1;
+            carry_pos = D.carry_pos;
+            // range-relative chunk of the first / last kept byte (lanes without
+            // a segment: never in a window), and the byte bounds there
+            const uint32_t sc = li ? (uint32_t)((a_abs - XB) >> 4) : 0xffffffffu;
+            const uint32_t ec = li ? (uint32_t)((a_end - XB) >> 4) : 0xffffffffu;
+            const uint32_t hb = (uint32_t)a_abs & 15u;        // bytes below the first
+            const uint32_t tb = ((uint32_t)a_end & 15u) + 1u;  // bytes up to the last
+            u32x4* swd = lds_swd[wid];
+            uint32_t* swf = lds_swf[wid];
+            uint32_t seg = 0;    // F(end) - F(start), modulo 2^32
+            uint32_t fbase = 0;  // F at the window's first chunk
+            // one window: chunk sums, the prefix F, staging ...
+            auto sweep_window = [&](const u32x4 (&v)[kSweep]) {
+              uint32_t sm[kSweep], I[kSweep];
+#pragma unroll
+              for (int q = 0; q < kSweep; ++q) {
+                sm[q] = chunk_halves(v[q], 0u);  // < 2^19
+                I[q] = sm[q];
+              }
+              wave_scan_add_n<kSweep>(I);
+#pragma unroll
+              for (int q = 0; q < kSweep; ++q) {
+                swd[q * 64 + lane] = v[q];
+                swf[q * 64 + lane] = fbase + I[q] - sm[q];
+                fbase += readlane_u32(I[q], 63);
+              }
+              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            };
+            // ... then the segments whose first / last kept byte lies in it
+            auto sweep_eval = [&](uint32_t w0) {
+              const uint32_t js = sc - w0, je = ec - w0;
+              if (js < (uint32_t)kSwCh) seg -= chunk_halves_masked(swd[js], lut.m[hb], swf[js]);
+              if (je < (uint32_t)kSwCh) seg += chunk_halves_masked(swd[je], lut.m[tb], swf[je]);
+              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            };
+            if constexpr (!kSweepDbl) {
+              for (uint32_t w0 = 0; w0 < span; w0 += (uint32_t)kSwCh) {
+                sweep_window(va);
+                // the next window's loads fly while this one's segments are read
+                if (w0 + (uint32_t)kSwCh < span) sweep_load(va, w0 + (uint32_t)kSwCh);
+                sweep_eval(w0);
+              }
+            } else {
+              // two register sets, two windows in flight: window w + 1 is
+              // loading while window w is summed and scanned (no copy between
+              // the sets: a copy would wait for the load it copies)
+              for (uint32_t w0 = 0; w0 < span; w0 += 2u * (uint32_t)kSwCh) {
+                sweep_window(va);
+                sweep_eval(w0);
+                if (w0 + (uint32_t)kSwCh >= span) break;
+                if (w0 + 2u * (uint32_t)kSwCh < span) sweep_load(va, w0 + 2u * (uint32_t)kSwCh);
+                sweep_window(vb);
+                sweep_eval(w0 + (uint32_t)kSwCh);
+                if (w0 + 3u * (uint32_t)kSwCh < span) sweep_load(vb, w0 + 3u * (uint32_t)kSwCh);
+              }
+            }
+            if (li) atomicAdd(&acc[D.meta], (unsigned long long)seg);
+            continue;
+          }
+        }
+      }
+      const Desc D = describe();
+      carry_slot1 = D.carry_slot1;
+      carry_pos = D.carry_pos;
+      const uint32_t eff = D.eff, head = D.head, nch = D.nch, meta = D.meta;
+      const uint64_t c0 = D.c0;
       const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
       // --- long segments: one wave-wide span each -------------------------
       const bool is_long =
@@ -293,96 +426,6 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       const uint64_t lm_list = __ballot(nch_l != 0);
       if (lm_list == 0) continue;
       const int lf = (int)__builtin_ctzll(lm_list);
-      // --- the address sweep ------------------------------------------------
-      if constexpr (kSweep > 0) {
-        const bool li = nch_l != 0;
-        const uint64_t a_abs = reinterpret_cast<uintptr_t>(base) + ao;  // first kept byte
-        const uint64_t a_end = a_abs + eff - 1;                         // last kept byte
-        const uint64_t X0 = readlane_u64((uint32_t)(a_abs >> 4), (uint32_t)(a_abs >> 36), lf);
-        // chunk numbers relative to the first list segment's, biased by 2^24:
-        // the round qualifies only if every one lies within 2^24 chunks of it
-        const uint64_t ds = (a_abs >> 4) - X0 + (1ull << 24);
-        const uint64_t de = (a_end >> 4) - X0 + (1ull << 24);
-        const bool inr = !li || (ds < (1ull << 25) && de < (1ull << 25));
-        const uint32_t rs = li ? (uint32_t)ds : 0xffffffffu;
-        const uint32_t re = li ? (uint32_t)de : 0u;
-        const uint32_t mn = ~readlane_u32(wave_scan<1, false>(~rs, 0u), 63);
-        const uint32_t mx = readlane_u32(wave_scan<1, false>(re, 0u), 63);
-        const uint32_t span = mx - mn + 1u;  // chunks of the range (valid when all inr)
-        if (__ballot(!inr) == 0 && span <= C + (C >> 2) + 64u) {
-          const uint64_t sb = (X0 + mn - (1ull << 24)) << 4;  // the range's first chunk
-          const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
-              reinterpret_cast<void*>(sb), 0, (int)(16u * span), 0x00020000);
-          // window-relative chunk of the first / last kept byte (lanes without
-          // a list segment: never in a window), and the byte bounds there
-          const uint32_t sc = li ? rs - mn : 0xffffffffu;
-          const uint32_t ec = li ? re - mn : 0xffffffffu;
-          const uint32_t hb = (uint32_t)a_abs & 15u;        // bytes below the first
-          const uint32_t tb = ((uint32_t)a_end & 15u) + 1u;  // bytes up to the last
-          u32x4* swd = lds_swd[wid];
-          uint32_t* swf = lds_swf[wid];
-          uint32_t seg = 0;    // F(end) - F(start), modulo 2^32
-          uint32_t fbase = 0;  // F at the window's first chunk
-          // chunks past the range read 0 (buffer range check): no clamp, no
-          // fault, no memory traffic -- so loads are issued unconditionally
-          auto sweep_load = [&](u32x4 (&v)[kSweep], uint32_t w0) {
-#pragma unroll
-            for (int q = 0; q < kSweep; ++q)
-              v[q] = __builtin_amdgcn_raw_buffer_load_b128(
-                  sr, (int)(16u * (w0 + (uint32_t)(q * 64 + lane))), 0, 2);
-          };
-          // one window: chunk sums, the prefix F, staging, then the
-          // segments whose first / last kept byte lies in it
-          auto sweep_window = [&](const u32x4 (&v)[kSweep], uint32_t w0) {
-            uint32_t s[kSweep], I[kSweep];
-#pragma unroll
-            for (int q = 0; q < kSweep; ++q) {
-              s[q] = chunk_halves(v[q], 0u);  // < 2^19
-              I[q] = s[q];
-            }
-            wave_scan_add_n<kSweep>(I);
-#pragma unroll
-            for (int q = 0; q < kSweep; ++q) {
-              swd[q * 64 + lane] = v[q];
-              swf[q * 64 + lane] = fbase + I[q] - s[q];
-              fbase += readlane_u32(I[q], 63);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          };
-          auto sweep_eval = [&](uint32_t w0) {
-            const uint32_t js = sc - w0, je = ec - w0;
-            if (js < (uint32_t)kSwCh) seg -= chunk_halves_masked(swd[js], lut.m[hb], swf[js]);
-            if (je < (uint32_t)kSwCh) seg += chunk_halves_masked(swd[je], lut.m[tb], swf[je]);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          };
-          u32x4 va_[kSweep];
-          sweep_load(va_, 0);
-          if constexpr (!kSweepDbl) {
-            for (uint32_t w0 = 0; w0 < span; w0 += (uint32_t)kSwCh) {
-              sweep_window(va_, w0);
-              // the next window's loads fly while this one's segments are read
-              if (w0 + (uint32_t)kSwCh < span) sweep_load(va_, w0 + (uint32_t)kSwCh);
-              sweep_eval(w0);
-            }
-          } else {
-            // two register sets, two windows in flight: window w + 1 is loading
-            // while window w is summed and scanned (no copy between the sets:
-            // a copy would wait for the load it copies)
-            u32x4 vb_[kSweep];
-            for (uint32_t w0 = 0; w0 < span; w0 += 2u * (uint32_t)kSwCh) {
-              sweep_load(vb_, w0 + (uint32_t)kSwCh);
-              sweep_window(va_, w0);
-              sweep_eval(w0);
-              sweep_load(va_, w0 + 2u * (uint32_t)kSwCh);
-              if (w0 + (uint32_t)kSwCh >= span) break;
-              sweep_window(vb_, w0 + (uint32_t)kSwCh);
-              sweep_eval(w0 + (uint32_t)kSwCh);
-            }
-          }
-          if (li) atomicAdd(&acc[meta], (unsigned long long)seg);
-          continue;
-        }
-      }
       const uint64_t R0 = readlane_u64(c0_lo, c0_hi, lf);
       const uint64_t rel = c0 - R0 + (1ull << 31);  // R0 - 2 GiB .. R0 + 2 GiB
       const bool window = __ballot(nch_l != 0 && rel >= (1ull << 32) - (1ull << 16)) == 0;

@@ -326,4 +326,10 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
 }
 
+// Lane i gets lane i-1's x (DPP wave_shr:1; lane 0 gets 0).  Needs all 64
+// lanes active.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, true);
+}
+
 }  // namespace uinet

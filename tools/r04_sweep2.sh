@@ -1,10 +1,12 @@
 #!/usr/bin/env bash
-# Round 4, second look at the sweep: the 2-pass windows without spills (6
-# waves), interleaved A/B against the chunk list, and SQ counters of the
+# Round 4, sweep v2 (early window loads from the raw descriptors, monotone +
+# no-hole rounds only): GPU parity, interleaved A/B against the chunk list, and SQ counters of the
 # chunk list (chains_sweep 0) vs the sweep (2, 4) on config 3.
 set -u
 TAG=${TAG:-r04b}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+timeout -k 10 600 python -u -m pytest tests/test_chains_sweep.py tests/test_chains32.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_sweep.log 2>&1
+rc=$?; tail -n 1 $OUT/pytest_sweep.log; [ $rc -eq 0 ] || { echo FATAL $rc; exit $rc; }
 for c in 3 3tx; do
   timeout -k 10 300 python -u tools/ab.py --config $c --rounds 6 --variants chains_sweep=0 chains_sweep=2 chains_sweep=3 chains_sweep=4 \
      chains_sweep=0,desc=1 chains_sweep=2,desc=1 chains_sweep=4,desc=1 > $OUT/ab_c$c.json 2> $OUT/ab_c$c.err
