@@ -87,7 +87,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v == 0 || v == 1; }},
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
-      {"chains_sweep", &TuningLive::chains_sweep, [](int v) { return v == 0 || (v >= 2 && v <= 4); }},
+      {"chains_sweep", &TuningLive::chains_sweep, [](int v) { return v == 0 || (v >= 2 && v <= 6); }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;

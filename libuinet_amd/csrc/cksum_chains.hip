@@ -116,7 +116,7 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 // is < 16 KiB, its weighted sum < 2^29).  One u64 LDS atomic per segment puts
 // it into its (packet, parity) bin.  Rounds that do not qualify (segments
 // scattered over more than 1.25x their own chunks) take the chunk list below.
-template <int kPass, int kTile, int kSweep, bool kSweepDbl, typename OffT, typename LenT>
+template <int kPass, int kTile, int kSweep, int kSweepMode, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
                                                        const LenT* __restrict__ seg_len,
@@ -195,6 +195,47 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
     }
   };
 
+  // The address sweep's plan for a round from its raw descriptors (segment
+  // offset `so`, length `l` per lane): true, with the range's first chunk
+  // address XB and its chunk count, when the round qualifies (see the round
+  // loop).  All 64 lanes must be active.
+  auto sweep_plan = [&](uint64_t so, uint32_t l, uint64_t& XB, uint32_t& span) -> bool {
+    const uint32_t lthr = (long_ch != 0 && long_ch < kListMax) ? long_ch : kListMax;
+    const uint64_t a0 = reinterpret_cast<uintptr_t>(base) + so;
+    const uint32_t rnch = l ? (uint32_t)(((a0 + l - 1) >> 4) - (a0 >> 4)) + 1u : 0u;
+    const bool el = l != 0;
+    const uint64_t em = __ballot(el);
+    if (em == 0 || __ballot(rnch >= lthr) != 0) return false;
+    const int fl = (int)__builtin_ctzll(em);
+    XB = readlane_u64((uint32_t)a0, (uint32_t)(a0 >> 32), fl) & ~15ull;
+    const uint64_t d = a0 - XB;  // huge when below XB: fails the order test
+    const bool near = d < (1ull << 30);
+    const uint32_t rs = el ? (uint32_t)d : 0u;
+    const uint32_t re = el ? rs + l : 0u;
+    const uint32_t ms = wave_scan<1, false>(rs, 0u);  // max start so far
+    const uint32_t me = wave_scan<1, false>(re, 0u);  // max end so far
+    const uint32_t ms_prev = wave_shr1(ms), me_prev = wave_shr1(me);
+    const bool bad = el && (!near || rs < ms_prev || (rs > me_prev && rs - me_prev >= 4096u));
+    const uint32_t C0 = readlane_u32(wave_scan<0, false>(rnch, 0u), 63);
+    span = ((readlane_u32(me, 63) - 1u) >> 4) + 1u;
+    return __ballot(bad) == 0 && span <= C0 + (C0 >> 2) + 64u;
+  };
+  auto sweep_rsrc = [&](uint64_t XB, uint32_t span) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(XB), 0, (int)(16u * span),
+                                             0x00020000);
+  };
+  // chunks past the range read 0 (buffer range check): no clamp, no fault, no
+  // memory traffic -- so window loads are issued unconditionally
+  auto sweep_load = [&](u32x4 (&v)[kSweep > 0 ? kSweep : 1], __amdgpu_buffer_rsrc_t sr,
+                        uint32_t w0) {
+#pragma unroll
+    for (int q = 0; q < (kSweep > 0 ? kSweep : 1); ++q)
+      v[q] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(16u * (w0 + (uint32_t)(q * 64 + lane))),
+                                                   0, 2);
+  };
+  (void)sweep_plan;
+  (void)sweep_rsrc;
+  (void)sweep_load;
   for (uint32_t t = blockIdx.x * kWaves + wid; t < tiles; t += wstride) {
     const uint32_t P0 = t * kTile;
     const int np = (int)min((uint32_t)kTile, n - P0);
@@ -216,10 +257,12 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       l_next = s < S1 ? (uint32_t)seg_len[sc] : 0u;
     };
     if (S0 < S1) fetch(S0);
+    u32x4 sw_va[kSweep > 0 ? kSweep : 1];  // the address sweep's window registers
+    (void)sw_va;
     for (uint32_t r0 = S0; r0 < S1; r0 += 64) {
       // --- descriptor round: one segment per lane -------------------------
-      const uint64_t so = so_next;
-      const uint32_t l = l_next;
+      uint64_t so = so_next;
+      uint32_t l = l_next;
       if (r0 + 64 < S1) fetch(r0 + 64);
       // The round's per-segment work: packet slot, chain position, the clip
       // to [skip, len), chunk count, bin.  It reads the carries of the
@@ -262,59 +305,37 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       };
       // --- the address sweep -------------------------------------------------
       // Decided first from the raw descriptors alone (before the clip), so the
-      // range's first windows load while `describe` runs.  The round
-      // qualifies when it holds no long segment and its segments, in lane
-      // order, start at non-decreasing addresses, leave no hole of 4 KiB or
-      // more between them (every byte the sweep reads then shares a 4-KiB page
-      // with a segment byte: nothing unmapped is touched), and fill at least
-      // 4/5 of their range.  Then every list segment's kept bytes [a, a + eff)
-      // must lie in it (they do, clipping only shrinks a segment), else the
-      // round is described again and takes the chunk list.
+      // range's first windows load while `describe` runs (kSweepMode 2: the
+      // previous round already issued them under its own last window).  The
+      // round qualifies when it holds no long segment and its segments, in
+      // lane order, start at non-decreasing addresses, leave no hole of 4 KiB
+      // or more between them (every byte the sweep reads then shares a 4-KiB
+      // page with a segment byte: nothing unmapped is touched), and fill at
+      // least 4/5 of their range.  Then every list segment's kept bytes
+      // [a, a + eff) must lie in it (they do, clipping only shrinks a
+      // segment), else the round is described again and takes the chunk list.
       if constexpr (kSweep > 0) {
-        const uint32_t lthr = (long_ch != 0 && long_ch < kListMax) ? long_ch : kListMax;
-        const uint64_t a0 = reinterpret_cast<uintptr_t>(base) + so;
-        const uint32_t rnch = l ? (uint32_t)(((a0 + l - 1) >> 4) - (a0 >> 4)) + 1u : 0u;
-        const bool el = l != 0;
-        const uint64_t em = __ballot(el);
-        bool ok = em != 0 && __ballot(rnch >= lthr) == 0;
-        uint64_t XB = 0;
-        uint32_t span = 0;
-        if (ok) {
-          const int fl = (int)__builtin_ctzll(em);
-          XB = readlane_u64((uint32_t)a0, (uint32_t)(a0 >> 32), fl) & ~15ull;
-          const uint64_t d = a0 - XB;  // huge when below XB: fails the order test
-          const bool near = d < (1ull << 30);
-          const uint32_t rs = el ? (uint32_t)d : 0u;
-          const uint32_t re = el ? rs + l : 0u;
-          const uint32_t ms = wave_scan<1, false>(rs, 0u);  // max start so far
-          const uint32_t me = wave_scan<1, false>(re, 0u);  // max end so far
-          const uint32_t ms_prev = wave_shr1(ms), me_prev = wave_shr1(me);
-          const bool bad =
-              el && (!near || rs < ms_prev || (rs > me_prev && rs - me_prev >= 4096u));
-          const uint32_t C0 = readlane_u32(wave_scan<0, false>(rnch, 0u), 63);
-          span = ((readlane_u32(me, 63) - 1u) >> 4) + 1u;
-          ok = __ballot(bad) == 0 && span <= C0 + (C0 >> 2) + 64u;
-        }
-        if (ok) {
-          const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
-              reinterpret_cast<void*>(XB), 0, (int)(16u * span), 0x00020000);
-          // chunks past the range read 0 (buffer range check): no clamp, no
-          // fault, no memory traffic -- so loads are issued unconditionally
-          auto sweep_load = [&](u32x4 (&v)[kSweep], uint32_t w0) {
-#pragma unroll
-            for (int q = 0; q < kSweep; ++q)
-              v[q] = __builtin_amdgcn_raw_buffer_load_b128(
-                  sr, (int)(16u * (w0 + (uint32_t)(q * 64 + lane))), 0, 2);
-          };
-          u32x4 va[kSweep], vb[kSweepDbl ? kSweep : 1];
-          sweep_load(va, 0);
-          if constexpr (kSweepDbl) sweep_load(vb, (uint32_t)kSwCh);
-          const Desc D = describe();
-          const bool li = D.nch != 0;
-          const uint64_t a_abs = reinterpret_cast<uintptr_t>(base) + D.ao;  // first kept byte
-          const uint64_t a_end = a_abs + D.eff - 1;                         // last kept byte
-          const bool in = !li || (a_abs - XB < 16ull * span && a_end - XB < 16ull * span);
-          if (__ballot(!in) == 0) {
+        uint64_t XB;
+        uint32_t span;
+        bool generic = false;  // this round failed the check after describe
+        if (sweep_plan(so, l, XB, span)) {
+          sweep_load(sw_va, sweep_rsrc(XB, span), 0);
+          // Sweep rounds back to back; in mode 2 each round's first window is
+          // issued under the previous round's last one.  The window registers
+          // stay live only inside this loop, never across the chunk list.
+          while (true) {
+            const __amdgpu_buffer_rsrc_t sr = sweep_rsrc(XB, span);
+            u32x4 vb[kSweepMode == 1 ? kSweep : 1];
+            if constexpr (kSweepMode == 1) sweep_load(vb, sr, (uint32_t)kSwCh);
+            const Desc D = describe();
+            const bool li = D.nch != 0;
+            const uint64_t a_abs = reinterpret_cast<uintptr_t>(base) + D.ao;  // first kept byte
+            const uint64_t a_end = a_abs + D.eff - 1;                         // last kept byte
+            const bool in = !li || (a_abs - XB < 16ull * span && a_end - XB < 16ull * span);
+            if (__ballot(!in) != 0) {
+              generic = true;
+              break;
+            }
             carry_slot1 = D.carry_slot1;
             carry_pos = D.carry_pos;
             // range-relative chunk of the first / last kept byte (lanes without
@@ -351,11 +372,20 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
               if (je < (uint32_t)kSwCh) seg += chunk_halves_masked(swd[je], lut.m[tb], swf[je]);
               __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             };
-            if constexpr (!kSweepDbl) {
+            bool next = false;  // the next round's first window is loading
+            uint64_t nxb = 0;
+            uint32_t nspan = 0;
+            if constexpr (kSweepMode != 1) {
               for (uint32_t w0 = 0; w0 < span; w0 += (uint32_t)kSwCh) {
-                sweep_window(va);
-                // the next window's loads fly while this one's segments are read
-                if (w0 + (uint32_t)kSwCh < span) sweep_load(va, w0 + (uint32_t)kSwCh);
+                sweep_window(sw_va);
+                // the next window's loads fly while this one's segments are
+                // read; under the last window, the next round's first
+                if (w0 + (uint32_t)kSwCh < span) {
+                  sweep_load(sw_va, sr, w0 + (uint32_t)kSwCh);
+                } else if (kSweepMode == 2 && r0 + 64 < S1) {
+                  next = sweep_plan(so_next, l_next, nxb, nspan);
+                  if (next) sweep_load(sw_va, sweep_rsrc(nxb, nspan), 0);
+                }
                 sweep_eval(w0);
               }
             } else {
@@ -363,18 +393,27 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
               // loading while window w is summed and scanned (no copy between
               // the sets: a copy would wait for the load it copies)
               for (uint32_t w0 = 0; w0 < span; w0 += 2u * (uint32_t)kSwCh) {
-                sweep_window(va);
+                sweep_window(sw_va);
                 sweep_eval(w0);
                 if (w0 + (uint32_t)kSwCh >= span) break;
-                if (w0 + 2u * (uint32_t)kSwCh < span) sweep_load(va, w0 + 2u * (uint32_t)kSwCh);
+                if (w0 + 2u * (uint32_t)kSwCh < span)
+                  sweep_load(sw_va, sr, w0 + 2u * (uint32_t)kSwCh);
                 sweep_window(vb);
                 sweep_eval(w0 + (uint32_t)kSwCh);
-                if (w0 + 3u * (uint32_t)kSwCh < span) sweep_load(vb, w0 + 3u * (uint32_t)kSwCh);
+                if (w0 + 3u * (uint32_t)kSwCh < span) sweep_load(vb, sr, w0 + 3u * (uint32_t)kSwCh);
               }
             }
             if (li) atomicAdd(&acc[D.meta], (unsigned long long)seg);
-            continue;
+            if (!next) break;
+            // on to the next round, inside this loop
+            r0 += 64;
+            so = so_next;
+            l = l_next;
+            if (r0 + 64 < S1) fetch(r0 + 64);
+            XB = nxb;
+            span = nspan;
           }
+          if (!generic) continue;
         }
       }
       const Desc D = describe();
@@ -554,17 +593,22 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
-#define LF(P, T, S, D)                                                                       \
-  UINET_LAUNCH((k_chains_pipe<P, T, S, D, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0,   \
+#define LF(P, T, S, M)                                                                       \
+  UINET_LAUNCH((k_chains_pipe<P, T, S, M, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0,   \
                stream, b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
   // chains_sweep: 0 off; 2 / 4 = windows of 2 / 4 passes; 3 = windows of 2
-  // passes, two in flight
+  // passes, two in flight; 5 / 6 = windows of 4 / 2 passes, each round's
+  // first window issued under the previous round's last
 #define LFS(P, T)                                  \
   do {                                             \
-    if (tn.chains_sweep == 4) LF(P, T, 4, false);  \
-    else if (tn.chains_sweep == 3) LF(P, T, 2, true); \
-    else if (tn.chains_sweep == 2) LF(P, T, 2, false); \
-    else LF(P, T, 0, false);                       \
+    switch (tn.chains_sweep) {                     \
+      case 2: LF(P, T, 2, 0); break;               \
+      case 3: LF(P, T, 2, 1); break;               \
+      case 4: LF(P, T, 4, 0); break;               \
+      case 5: LF(P, T, 4, 2); break;               \
+      case 6: LF(P, T, 2, 2); break;               \
+      default: LF(P, T, 0, 0); break;              \
+    }                                              \
   } while (0)
   if (tile == 8) {
     if (tn.chains_pass == 4) LFS(4, 8);

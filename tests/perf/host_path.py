@@ -31,25 +31,34 @@ def best(fn, reps=5):
 
 
 def main():
-    R = oracle.Reference() if oracle.have_reference() else None
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="c2,c3", help="c2 (65,536 and 1 M x 1500 B), c3")
+    ap.add_argument("--no-reference", action="store_true", help="engine only (A/B runs)")
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    R = oracle.Reference() if oracle.have_reference() and not a.no_reference else None
     res = {}
     shapes = []
-    for n in (65536, 1 << 20):
+    for n in ((65536, 1 << 20) if "c2" in a.shapes else ()):
         arena = aligned_empty(1500 * n + 64)
         splitmix64_bytes(arena.size, 2, out=arena)
         ch = MbufChains.contiguous(arena, 1500 * np.arange(n), 1500)
         shapes.append((f"c2_{n}", arena, ch, 1500, 0, n * 1500))
-    c3 = build_config3(1 << 18, seed=3)
-    ch3 = MbufChains(c3["arena"], c3["seg_off"], c3["seg_len"], c3["pkt_seg"])
-    shapes.append(("c3_262144", c3["arena"], ch3, c3["lens"], 20, int((c3["lens"] - 20).sum())))
+    if "c3" in a.shapes:
+        c3 = build_config3(1 << 18, seed=3)
+        ch3 = MbufChains(c3["arena"], c3["seg_off"], c3["seg_len"], c3["pkt_seg"])
+        shapes.append(("c3_262144", c3["arena"], ch3, c3["lens"], 20,
+                       int((c3["lens"] - 20).sum())))
     for name, arena, ch, ln, sk, nbytes in shapes:
         gib = nbytes / 2**30
         u.in_cksum_skip_batch(ch.heads, ln, sk)
-        t_stage, r_stage = best(lambda: u.in_cksum_skip_batch(ch.heads, ln, sk))
+        t_stage, r_stage = best(lambda: u.in_cksum_skip_batch(ch.heads, ln, sk), a.reps)
         u.register_host(arena)
         try:
             u.in_cksum_skip_batch(ch.heads, ln, sk)
-            t_zc, r_zc = best(lambda: u.in_cksum_skip_batch(ch.heads, ln, sk))
+            t_zc, r_zc = best(lambda: u.in_cksum_skip_batch(ch.heads, ln, sk), a.reps)
         finally:
             u.unregister_host(arena)
         e = {"staging_gibs": round(gib / t_stage, 2), "zero_copy_gibs": round(gib / t_zc, 2),

@@ -89,7 +89,7 @@ def with_knobs(knobs, fn):
 
 
 @pytest.mark.parametrize("shape", ["in", "shuffled", "overlap", "mixed"])
-@pytest.mark.parametrize("sweep", [0, 2, 3, 4])
+@pytest.mark.parametrize("sweep", [0, 2, 3, 4, 5, 6])
 def test_sweep_layouts(torch_dev, ora, shape, sweep):
     torch = torch_dev
     rng = np.random.default_rng(12000 + 10 * sweep + len(shape))
@@ -104,7 +104,7 @@ def test_sweep_layouts(torch_dev, ora, shape, sweep):
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("sweep", [2, 3, 4])
+@pytest.mark.parametrize("sweep", [2, 3, 4, 5, 6])
 @pytest.mark.parametrize("tile,cpass,long_ch", [(8, 2, 128), (32, 4, 128), (32, 2, 16), (8, 4, 0)])
 def test_sweep_geometries(torch_dev, ora, sweep, tile, cpass, long_ch):
     """Dense rounds at both tile sizes and batch widths, with long segments
@@ -124,7 +124,7 @@ def test_sweep_geometries(torch_dev, ora, sweep, tile, cpass, long_ch):
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("sweep", [2, 3, 4])
+@pytest.mark.parametrize("sweep", [2, 3, 4, 5, 6])
 def test_sweep_extremes(torch_dev, ora, sweep):
     """All-0x00 and all-0xff bytes (0 vs 0xffff after the fold), rounds of 64
     one-byte segments, segments ending on the arena's last byte, and rounds
@@ -162,7 +162,7 @@ def test_sweep_extremes(torch_dev, ora, sweep):
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("sweep", [0, 2, 3, 4])
+@pytest.mark.parametrize("sweep", [0, 2, 3, 4, 5, 6])
 def test_sweep_config3_slice(torch_dev, ora, sweep):
     """Config 3's own layout (m_fragment chains, in order, 0-7-B gaps) at
     65,536 packets, wide and packed descriptors."""
