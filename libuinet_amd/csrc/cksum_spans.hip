@@ -519,17 +519,6 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
   constexpr uint32_t kRoundB = 64u * U;  // bytes of a span one round covers
   constexpr uint32_t kWavesPB = kBlock / 64;
   __shared__ u32x4 lut_m[34];  // the split mask table (see k_spans_lean)
-  // the address sweep's staging, one window of kSW passes per wave (spans API)
-  constexpr int kSW = 4;
-  constexpr int kSWW = kStrided ? 1 : (int)kWavesPB;
-  constexpr int kSWC = kStrided ? 1 : 64 * kSW;
-#ifdef UINET_QUAD_NOSWEEP
-  __shared__ u32x4 sw_d[1][1];
-  __shared__ uint32_t sw_f[1][1];
-#else
-  __shared__ u32x4 sw_d[kSWW][kSWC];
-  __shared__ uint32_t sw_f[kSWW][kSWC];
-#endif
   auto mask_se = [&](int s_, int e_) -> u32x4 {
     return lut_m[clampi(e_, 0, 16)] & lut_m[17 + clampi(s_, 0, 16)];
   };
@@ -661,48 +650,6 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
         finish(full_sum(y), y, j);
       }
   };
-  // A super-step whose 64 spans lie in one dense address range (in order,
-  // no hole of 4 KiB, >= 4/5 filled: sweep_plan) is read as plain chunks
-  // with a running prefix (cksum_device.h, "The address sweep") instead of
-  // quads: a span off 16-B alignment then costs no extra chunk slot.  Lane i
-  // holds packet p + i's result in `res` afterwards.  Spans API only.
-  auto sweep_super = [&](const B& c, uint32_t p0) -> bool {
-#ifdef UINET_QUAD_NOSWEEP  // lab A/B build only (tools/r04_quad.sh): quads everywhere
-    if constexpr (true) {
-#else
-    if constexpr (kStrided) {
-#endif
-      return false;
-    } else {
-      const uint32_t l = p0 + lane < n ? c.l : 0u;
-      const uint64_t a0 =
-          reinterpret_cast<uintptr_t>(base) + (((uint64_t)c.ohi << 32) | c.olo);
-      uint64_t XB;
-      uint32_t span;
-      if (!sweep_plan(a0, l, 1024u, XB, span)) return false;
-      const __amdgpu_buffer_rsrc_t sr = sweep_rsrc(XB, span);
-      u32x4 v[kSW];
-      sweep_load<kSW>(v, sr, 0u, lane);
-      SweepSpan<kSW> sp;
-      sp.init(sw_d[threadIdx.x >> 6], sw_f[threadIdx.x >> 6], lut_m, a0, l, XB);
-      for (uint32_t w0 = 0; w0 < span; w0 += 64u * kSW) {
-        sp.window(v, lane);
-        if (w0 + 64u * kSW < span) sweep_load<kSW>(v, sr, w0 + 64u * kSW, lane);
-        sp.eval(w0);
-      }
-      uint32_t x = fold16_32(sp.seg);
-      const uint32_t rot = ((kParity ? c.lp : 0u) ^ (uint32_t)a0) & 1u;  // in_cksum.c:222-225
-      x = fold16_32(x << (8u * rot));
-      if constexpr (kSeed) x = fold16_32(x + fold16_32(c.sd));
-      uint32_t r = x;
-      if (!(flags & UINET_CKSUM_F_NO_COMPLEMENT)) {
-        r = ~x & 0xffffu;
-        if ((flags & UINET_CKSUM_F_UDP) && r == 0) r = 0xffff;  // ip_output.c:962-963
-      }
-      res = r;
-      return true;
-    }
-  };
   // lanes past the batch address past the end of the buffer resource: the
   // hardware drops their writes
   auto flush = [&](uint32_t p0) {
@@ -737,16 +684,6 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
   // The four steps of a full super-step at p (step 0 in flight in A), the
   // next super-step's step 0 (block nx) issued under the last sum.
   auto super = [&](const B& c, const B& nx) {
-    if constexpr (!kStrided) {
-      if (sweep_super(c, p)) {
-        // the next super-step's step 0 in flight in A, as the quads expect
-        zA = geo(nx, p + S, 0);
-        load(zA, vA);
-        flush(p);
-        p += S;
-        return;
-      }
-    }
     uint32_t pend = 0;
     zB = geo(c, p, 1);
     load(zB, vB);  // step 1 in flight while step 0 is summed
@@ -766,12 +703,6 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
   };
   // The last super-step: J live steps (1..4), step 0 in flight in A.
   auto last = [&](const B& c) {
-    if constexpr (!kStrided) {
-      if (sweep_super(c, p)) {
-        flush(p);
-        return;
-      }
-    }
     uint32_t pend = 0;
     const uint32_t J = min((n - p + 15u) / 16u, 4u);
     if (J == 1) {
