@@ -131,6 +131,13 @@ int in6_cksum_pseudo(struct ip6_hdr *ip6, uint32_t len, uint8_t nxt,
 /* Result flags for the batch/device entry points. */
 #define UINET_CKSUM_F_UDP           0x1u /* 0 -> 0xffff (ip_output.c:962-963) */
 #define UINET_CKSUM_F_NO_COMPLEMENT 0x2u /* return the folded sum, in_pseudo-style */
+/* A performance hint for uinet_cksum_chains / uinet_cksum_chains32 (never
+ * changes results): the batch's segments lie mostly in address order, close
+ * together -- mbufs carved one after another out of large buffers.  The
+ * chain kernel then reads such runs of segments as plain 16-B chunks (the
+ * address sweep) and checks every 64-segment round before it does; a round
+ * that is not ordered takes a slower path, so a wrong hint costs time only. */
+#define UINET_CKSUM_F_ORDERED       0x4u
 
 /* Engine version string and HIP diagnostics. */
 const char *uinet_cksum_version(void);
@@ -150,10 +157,6 @@ int uinet_cksum_device_ok(void);
  *   "chains_long"     chain segments of at least this many 16-B chunks are
  *                     streamed wave-wide; 0 = never, else >= 16 (default 128)
  *   "chains_tile"     packets per wave in the chain kernel: 0 = auto, 8, 32
- *   "chains_sweep"    chain kernel: descriptor rounds whose segments lie in
- *                     one dense address range are read as plain chunks with
- *                     a running prefix, windows of 2 (default) or 4 x 64
- *                     chunks; 0 = every round through the chunk list
  *   "xcd_remap"       span kernels: give each XCD a contiguous band of
  *                     packets (1, default) or plain block order (0)
  *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
@@ -176,9 +179,8 @@ int uinet_cksum_device_ok(void);
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU,
  * UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG, UINET_CKSUM_CHAINS_TILE,
  * UINET_CKSUM_XCD_REMAP, UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF,
- * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_PIPE, UINET_CKSUM_HOST_PIN,
- * UINET_CKSUM_MULTI_GATHER and UINET_CKSUM_CHAINS_SWEEP set the initial
- * values. */
+ * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_PIPE, UINET_CKSUM_HOST_PIN and
+ * UINET_CKSUM_MULTI_GATHER set the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
 /* ------------------------------------------------------------------------ */

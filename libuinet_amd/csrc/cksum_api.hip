@@ -64,7 +64,7 @@ void note_kernel(const void* host_stub) { t_last_kernel = host_stub; }
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_pass{2}, host_threads{8}, chains_long{128},
       chains_tile{0}, xcd_remap{1}, walk_prefetch{1}, spans_geo{0}, spans_pipe{1},
-      host_pin{0}, multi_gather{0}, chains_sweep{2};
+      host_pin{0}, multi_gather{0};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -87,7 +87,6 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v == 0 || v == 1; }},
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
-      {"chains_sweep", &TuningLive::chains_sweep, [](int v) { return v == 0 || (v >= 2 && v <= 6); }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -106,7 +105,6 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_GEO", "spans_geo"},
         {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},
         {"UINET_CKSUM_HOST_PIN", "host_pin"},          {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},
-        {"UINET_CKSUM_CHAINS_SWEEP", "chains_sweep"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -136,7 +134,6 @@ Tuning tuning() {
   x.spans_pipe = ld(t.spans_pipe);
   x.host_pin = ld(t.host_pin);
   x.multi_gather = ld(t.multi_gather);
-  x.chains_sweep = ld(t.chains_sweep);
   return x;
 }
 

@@ -8,33 +8,36 @@
 // nothing, a short chain sums what it has), with the logical parity counted
 // from `skip`.  len == NULL means "the whole chain", skip == NULL means 0.
 //
-// k_chains_pipe (default) -- a wave owns a tile of 32 consecutive packets and
-// therefore a contiguous range of segments, processed in descriptor rounds of
-// 64 segments (one per lane):
-//   * per segment: its packet slot (LDS start markers + a DPP max-scan), its
-//     chain position (a DPP add-scan of the lengths minus a max-scan of the
-//     packet-start positions, carried across rounds), the clip to
-//     [skip, len), its chunk count;
-//   * the round's segments become one concatenated list of 16-byte chunks
-//     (DPP scan of the chunk counts) that the wave sweeps 64 chunks per pass,
-//     kPass passes per batch -- every load is a dense 1 KiB whatever the
-//     segment lengths;
-//   * a chunk finds its segment by LDS start markers + a DPP max-scan, its
-//     bytes are masked with one ds_read_b128 from a 17x17 mask table;
-//   * chunk sums are binned per (packet, parity) with a plain DPP prefix sum
-//     P: the last lane of each run of equal bins adds +P to its bin and -P to
-//     the next run's bin (telescoping), into the wave's u64 LDS accumulators;
-//     each packet's odd-parity bin is byte-rotated once at the end;
-//   * long segments (>= long_ch chunks) skip the chunk list: the whole wave
-//     streams each one like a span and adds one wave-reduced sum to its bin;
-//   * software pipelining: each batch is issued one step before it is summed.
-// Tiles of 8 packets instead of 32 when the batch is small enough that 32
-// would leave too few waves to balance 256 CUs (e.g. jumbo frames).
-// Formulations measured and removed (code under profiles/r03/pruned/): a
-// serial walk (G lanes per packet, one segment after another), a bitmap
-// segment lookup (chains_variant 2), and k_chains_lean (LDS segment records,
-// bitmap lookup, copy-free two-batch pipeline at 8 waves per SIMD: 40 %
-// slower on config 3, profiles/r03/r03e/ab_c3.log).
+// Both kernels give a wave a tile of 32 consecutive packets (8 when the batch
+// is small), i.e. a contiguous range of segments, processed in descriptor
+// rounds of 64 segments (one per lane, `describe_round`): packet slot (LDS
+// start markers + a DPP max-scan), chain position (a DPP add-scan of the
+// lengths minus a max-scan of the packet-start positions, carried across
+// rounds), the clip to [skip, len), chunk count, (packet, parity) bin.  Long
+// segments (>= long_ch chunks) are streamed by the whole wave, one at a time
+// (`stream_long`).  Sums land in the wave's u64 LDS bins per (packet,
+// parity); each packet's odd-parity bin is byte-rotated once at the end.
+//
+// k_chains_pipe (default) -- the chunk list: a round's short segments become
+// one concatenated list of 16-byte chunks that the wave sweeps 64 chunks per
+// pass, so every load is a dense 1 KiB whatever the segment lengths; a chunk
+// finds its segment by LDS start markers + a DPP max-scan, is masked from a
+// 17x17 LDS table and binned by a telescoping DPP prefix sum; each batch of
+// passes is issued one step before it is summed.
+//
+// k_chains_sweep (UINET_CKSUM_F_ORDERED) -- the address sweep
+// (cksum_device.h): a round whose segments lie in one dense address range, in
+// order, is read as plain chunks with a running prefix F, two 4-KiB windows
+// in flight, and each segment is F(end) - F(start); the next round's first
+// windows load while it is described.  Other rounds take a light path (long
+// segments wave-wide, the rest lane by lane).
+//
+// Formulations measured and removed (code under profiles/r03/pruned/ and
+// profiles/r04/pruned/): a serial walk (G lanes per packet), a bitmap segment
+// lookup, k_chains_lean (LDS segment records), and the address sweep inside
+// k_chains_pipe with the chunk list as its fallback (one kernel's static LDS
+// and registers held every round to 5 waves per SIMD: config 3 +1.5 %, 3tx
+// -4 %, profiles/r04/r04b/).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -62,12 +65,95 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rsrc(const uint8_t* sba
                                            0x00020000);
 }
 __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-#ifdef UINET_CHAINS_LAB_NOLOAD  // tools/chains_lab ablation only: no packet-byte loads
-  (void)r;
-  return u32x4{off, off ^ 0x5a5a5a5au, off + 7u, off * 3u};
-#else
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2);
-#endif
+}
+
+// One descriptor round's per-segment work, one segment per lane (segment
+// r0 + lane: offset so, length l): the packet slot from the LDS start markers
+// of the tile's packets (`ps` = lane's packet's first segment, np packets),
+// the chain position, the clip to [skip, len) (lane's packet's k_skip /
+// k_len, read by slot), the chunk count and the (slot, rotation) bin.  It
+// reads the previous round's carries and returns the new ones.
+struct RoundDesc {
+  uint32_t slot, pos, eff, head, nch, rot, meta, carry_slot1, carry_pos;
+  uint64_t ao, c0;
+};
+__device__ __forceinline__ RoundDesc describe_round(uint32_t* pkmark, int lane, int np, uint32_t ps,
+                                                    uint32_t r0, uint64_t so, uint32_t l,
+                                                    uint32_t k_skip, uint32_t k_len,
+                                                    uint32_t carry_slot1, uint32_t carry_pos,
+                                                    const uint8_t* base) {
+  RoundDesc D;
+  const bool pk_in = lane < np && ps >= r0 && ps < r0 + 64;
+  if (pk_in) atomicMax(&pkmark[ps - r0], (uint32_t)lane + 1);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t pk = pkmark[lane];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (pk_in) pkmark[ps - r0] = 0;
+  const uint32_t slot1 = max(wave_scan<1, false>(pk, 0u), carry_slot1);
+  D.slot = slot1 - 1;
+  // chain position: T = carry_pos + exclusive prefix of the lengths never
+  // decreases along the lanes, so the max-scan of T at packet starts is T at
+  // this segment's packet start (0 while the packet of the previous round
+  // continues: its position is T itself)
+  const uint32_t T = carry_pos + wave_scan<0, false>(l, 0u) - l;
+  D.pos = T - wave_scan<1, false>(pk ? T : 0u, 0u);
+  D.carry_slot1 = __builtin_amdgcn_readlane(slot1, 63);
+  D.carry_pos = __builtin_amdgcn_readlane(D.pos + l, 63);
+  const uint32_t sk = __shfl(k_skip, (int)D.slot);
+  const uint32_t ln = __shfl(k_len, (int)D.slot);
+  const uint32_t lo = sk > D.pos ? min(sk - D.pos, l) : 0u;
+  const uint32_t hi = ln > D.pos ? min(ln - D.pos, l) : 0u;
+  D.eff = hi > lo ? hi - lo : 0u;
+  D.ao = so + lo;
+  D.head = D.eff ? (uint32_t)(reinterpret_cast<uintptr_t>(base + D.ao) & 15) : 0u;
+  // chunks touched, without forming head + eff (a u32 segment may be 4 GiB)
+  D.nch = D.eff ? (D.eff >> 4) + ((D.head + (D.eff & 15u) + 15u) >> 4) : 0u;
+  D.c0 = D.ao - D.head;
+  D.rot = ((D.pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(base + D.ao)) & 1u;
+  D.meta = (D.slot << 1) | D.rot;
+  return D;
+}
+
+// The round's long segments (lanes set in lm), one wave-wide span each:
+// kLongU chunks per lane in flight, one wave-reduced sum added to the
+// segment's bin.  sum(v, lo, hi) folds bytes [lo, hi) of a chunk (u64).
+template <typename SumFn>
+__device__ __forceinline__ void stream_long(uint64_t lm, const RoundDesc& D, const uint8_t* base,
+                                            int lane, unsigned long long* acc, SumFn sum) {
+  const uint32_t c0_lo = (uint32_t)D.c0, c0_hi = (uint32_t)(D.c0 >> 32);
+  for (; lm; lm &= lm - 1) {
+    const int s = (int)__builtin_ctzll(lm);
+    // head and length read separately: a segment may hold up to 4 GiB, more
+    // than one packed 32-bit word (eff << 4 | head) keeps
+    const uint32_t h = __builtin_amdgcn_readlane(D.head, s);
+    const uint32_t el = __builtin_amdgcn_readlane(D.eff, s);
+    const uint32_t mts = __builtin_amdgcn_readlane(D.meta, s);
+    const uint8_t* cb = base + (readlane_u64(c0_lo, c0_hi, s));
+    const uint32_t nc = __builtin_amdgcn_readlane(D.nch, s);
+    // chunk k keeps bytes [k ? 0 : h, k < nc - 1 ? 16 : last_end): only the
+    // first and last chunks are partial, so no byte position is formed
+    const uint32_t last_end = ((h + (el & 15u) + 15u) & 15u) + 1u;
+    uint64_t lsum = 0;
+    for (uint32_t k0 = 0; k0 < nc; k0 += 64 * kLongU) {
+      u32x4 v[kLongU];
+#pragma unroll
+      for (int u = 0; u < kLongU; ++u)
+        if (u == 0 || k0 + 64u * u < nc)
+          v[u] = load_chunk(cb + 16ull * min(k0 + (uint32_t)(u * 64 + lane), nc - 1));
+#pragma unroll
+      for (int u = 0; u < kLongU; ++u) {
+        if (u == 0 || k0 + 64u * u < nc) {
+          const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
+          const int lo_b = k == 0 ? (int)h : (k < nc ? 0 : 16);
+          const int hi_b = k + 1 < nc ? 16 : (k + 1 == nc ? (int)last_end : 0);
+          lsum += sum(v[u], lo_b, hi_b);
+        }
+      }
+    }
+    const uint32_t x = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(lsum), 0u), 63);
+    if (lane == 0) atomicAdd(&acc[mts], (unsigned long long)x);
+  }
 }
 
 // k_chains_pipe: the pipelining and addressing details.
@@ -100,23 +186,10 @@ __device__ __forceinline__ u32x4 load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32
 #ifdef UINET_CHAINS_WAVES
 #define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(UINET_CHAINS_WAVES)))
 #else
-#define UINET_CHAINS_OCC \
-  __attribute__((amdgpu_waves_per_eu(kPass == 2 ? (kSweep == 2 ? 6 : 7) : 1)))
+#define UINET_CHAINS_OCC __attribute__((amdgpu_waves_per_eu(kPass == 2 ? 7 : 1)))
 #endif
 
-// kSweep > 0 adds the address sweep (a descriptor round whose list segments
-// lie inside one dense address range, e.g. mbufs carved in order out of one
-// buffer): the wave reads that range as plain 16-B chunks, kSweep passes of
-// 64 per window, with no per-chunk segment lookup, mask or bin.  Each chunk
-// adds its whole 8-halfword sum to a running prefix F (one DPP scan per pass);
-// F and the chunk are staged in LDS for the window, and each segment's lane
-// reads, in the window holding its first and its last kept byte,
-//   F(x) = F(first byte of x's chunk) + (halves of x's chunk below x)
-// so the segment's sum is F(end) - F(start) (exact modulo 2^32: a list segment
-// is < 16 KiB, its weighted sum < 2^29).  One u64 LDS atomic per segment puts
-// it into its (packet, parity) bin.  Rounds that do not qualify (segments
-// scattered over more than 1.25x their own chunks) take the chunk list below.
-template <int kPass, int kTile, int kSweep, int kSweepMode, typename OffT, typename LenT>
+template <int kPass, int kTile, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const uint8_t* __restrict__ base,
                                                        const OffT* __restrict__ seg_off,
                                                        const LenT* __restrict__ seg_len,
@@ -136,9 +209,6 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
   // segment-start markers per batch, (lane + 1) << 8 | meta, and one spare slot
   // per lane that lanes without a start in the batch write (no exec mask)
   __shared__ uint16_t lds_mark[kWaves][kWin + 64];
-  constexpr int kSwCh = 64 * (kSweep > 0 ? kSweep : 1);  // chunks per sweep window
-  __shared__ u32x4 lds_swd[kSweep > 0 ? kWaves : 1][kSweep > 0 ? kSwCh : 1];   // window bytes
-  __shared__ uint32_t lds_swf[kSweep > 0 ? kWaves : 1][kSweep > 0 ? kSwCh : 1];  // F per chunk
   lut.init();
   for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
   for (int i = threadIdx.x; i < kWaves * (kWin + 64); i += blockDim.x) (&lds_mark[0][0])[i] = 0;
@@ -166,20 +236,10 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
   // The passes' chunk sums first, then their prefix sums side by side (the
   // DPP chains interleave: +1.3-3 % on config 3, profiles/r02/ab_lab/), then
   // the bin updates.
-#ifdef UINET_CHAINS_LAB_PAD  // tools/chains_lab only: N extra VALU per pass (is VALU the bound?)
-  uint32_t lab_pad = 0;
-#endif
   auto consume = [&](const u32x4 (&v)[kPass], const uint32_t (&key)[kPass]) {
     uint32_t P[kPass], sl[kPass], nx[kPass];
 #pragma unroll
     for (int q = 0; q < kPass; ++q) P[q] = lut.sum_oc_idx(v[q], key[q] & 0xffffu);  // < 2^19
-#ifdef UINET_CHAINS_LAB_PAD
-#pragma unroll
-    for (int q = 0; q < kPass; ++q)
-#pragma unroll
-      for (int i = 0; i < UINET_CHAINS_LAB_PAD; ++i)
-        asm volatile("v_add_u32 %0, %0, %1" : "+v"(lab_pad) : "v"(P[q]));
-#endif
 #pragma unroll
     for (int q = 0; q < kPass; ++q) {
       sl[q] = key[q] >> 16;
@@ -195,47 +255,6 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
     }
   };
 
-  // The address sweep's plan for a round from its raw descriptors (segment
-  // offset `so`, length `l` per lane): true, with the range's first chunk
-  // address XB and its chunk count, when the round qualifies (see the round
-  // loop).  All 64 lanes must be active.
-  auto sweep_plan = [&](uint64_t so, uint32_t l, uint64_t& XB, uint32_t& span) -> bool {
-    const uint32_t lthr = (long_ch != 0 && long_ch < kListMax) ? long_ch : kListMax;
-    const uint64_t a0 = reinterpret_cast<uintptr_t>(base) + so;
-    const uint32_t rnch = l ? (uint32_t)(((a0 + l - 1) >> 4) - (a0 >> 4)) + 1u : 0u;
-    const bool el = l != 0;
-    const uint64_t em = __ballot(el);
-    if (em == 0 || __ballot(rnch >= lthr) != 0) return false;
-    const int fl = (int)__builtin_ctzll(em);
-    XB = readlane_u64((uint32_t)a0, (uint32_t)(a0 >> 32), fl) & ~15ull;
-    const uint64_t d = a0 - XB;  // huge when below XB: fails the order test
-    const bool near = d < (1ull << 30);
-    const uint32_t rs = el ? (uint32_t)d : 0u;
-    const uint32_t re = el ? rs + l : 0u;
-    const uint32_t ms = wave_scan<1, false>(rs, 0u);  // max start so far
-    const uint32_t me = wave_scan<1, false>(re, 0u);  // max end so far
-    const uint32_t ms_prev = wave_shr1(ms), me_prev = wave_shr1(me);
-    const bool bad = el && (!near || rs < ms_prev || (rs > me_prev && rs - me_prev >= 4096u));
-    const uint32_t C0 = readlane_u32(wave_scan<0, false>(rnch, 0u), 63);
-    span = ((readlane_u32(me, 63) - 1u) >> 4) + 1u;
-    return __ballot(bad) == 0 && span <= C0 + (C0 >> 2) + 64u;
-  };
-  auto sweep_rsrc = [&](uint64_t XB, uint32_t span) {
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(XB), 0, (int)(16u * span),
-                                             0x00020000);
-  };
-  // chunks past the range read 0 (buffer range check): no clamp, no fault, no
-  // memory traffic -- so window loads are issued unconditionally
-  auto sweep_load = [&](u32x4 (&v)[kSweep > 0 ? kSweep : 1], __amdgpu_buffer_rsrc_t sr,
-                        uint32_t w0) {
-#pragma unroll
-    for (int q = 0; q < (kSweep > 0 ? kSweep : 1); ++q)
-      v[q] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(16u * (w0 + (uint32_t)(q * 64 + lane))),
-                                                   0, 2);
-  };
-  (void)sweep_plan;
-  (void)sweep_rsrc;
-  (void)sweep_load;
   for (uint32_t t = blockIdx.x * kWaves + wid; t < tiles; t += wstride) {
     const uint32_t P0 = t * kTile;
     const int np = (int)min((uint32_t)kTile, n - P0);
@@ -257,166 +276,13 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       l_next = s < S1 ? (uint32_t)seg_len[sc] : 0u;
     };
     if (S0 < S1) fetch(S0);
-    u32x4 sw_va[kSweep > 0 ? kSweep : 1];  // the address sweep's window registers
-    (void)sw_va;
     for (uint32_t r0 = S0; r0 < S1; r0 += 64) {
       // --- descriptor round: one segment per lane -------------------------
-      uint64_t so = so_next;
-      uint32_t l = l_next;
+      const uint64_t so = so_next;
+      const uint32_t l = l_next;
       if (r0 + 64 < S1) fetch(r0 + 64);
-      // The round's per-segment work: packet slot, chain position, the clip
-      // to [skip, len), chunk count, bin.  It reads the carries of the
-      // previous round and returns the new ones (the caller commits them).
-      struct Desc {
-        uint32_t slot, pos, eff, head, nch, rot, meta, carry_slot1, carry_pos;
-        uint64_t ao, c0;
-      };
-      auto describe = [&]() {
-        Desc D;
-        const bool pk_in = lane < np && ps >= r0 && ps < r0 + 64;
-        if (pk_in) atomicMax(&pkmark[ps - r0], (uint32_t)lane + 1);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const uint32_t pk = pkmark[lane];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (pk_in) pkmark[ps - r0] = 0;
-        const uint32_t slot1 = max(wave_scan<1, false>(pk, 0u), carry_slot1);
-        D.slot = slot1 - 1;
-        // chain position: T = carry_pos + exclusive prefix of the lengths never
-        // decreases along the lanes, so the max-scan of T at packet starts is
-        // T at this segment's packet start (0 while the packet of the previous
-        // round continues: its position is T itself)
-        const uint32_t T = carry_pos + wave_scan<0, false>(l, 0u) - l;
-        D.pos = T - wave_scan<1, false>(pk ? T : 0u, 0u);
-        D.carry_slot1 = __builtin_amdgcn_readlane(slot1, 63);
-        D.carry_pos = __builtin_amdgcn_readlane(D.pos + l, 63);
-        const uint32_t sk = __shfl(k_skip, (int)D.slot);
-        const uint32_t ln = __shfl(k_len, (int)D.slot);
-        const uint32_t lo = sk > D.pos ? min(sk - D.pos, l) : 0u;
-        const uint32_t hi = ln > D.pos ? min(ln - D.pos, l) : 0u;
-        D.eff = hi > lo ? hi - lo : 0u;
-        D.ao = so + lo;
-        D.head = D.eff ? (uint32_t)(reinterpret_cast<uintptr_t>(base + D.ao) & 15) : 0u;
-        // chunks touched, without forming head + eff (a u32 segment may be 4 GiB)
-        D.nch = D.eff ? (D.eff >> 4) + ((D.head + (D.eff & 15u) + 15u) >> 4) : 0u;
-        D.c0 = D.ao - D.head;
-        D.rot = ((D.pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(base + D.ao)) & 1u;
-        D.meta = (D.slot << 1) | D.rot;
-        return D;
-      };
-      // --- the address sweep -------------------------------------------------
-      // Decided first from the raw descriptors alone (before the clip), so the
-      // range's first windows load while `describe` runs (kSweepMode 2: the
-      // previous round already issued them under its own last window).  The
-      // round qualifies when it holds no long segment and its segments, in
-      // lane order, start at non-decreasing addresses, leave no hole of 4 KiB
-      // or more between them (every byte the sweep reads then shares a 4-KiB
-      // page with a segment byte: nothing unmapped is touched), and fill at
-      // least 4/5 of their range.  Then every list segment's kept bytes
-      // [a, a + eff) must lie in it (they do, clipping only shrinks a
-      // segment), else the round is described again and takes the chunk list.
-      if constexpr (kSweep > 0) {
-        uint64_t XB;
-        uint32_t span;
-        bool generic = false;  // this round failed the check after describe
-        if (sweep_plan(so, l, XB, span)) {
-          sweep_load(sw_va, sweep_rsrc(XB, span), 0);
-          // Sweep rounds back to back; in mode 2 each round's first window is
-          // issued under the previous round's last one.  The window registers
-          // stay live only inside this loop, never across the chunk list.
-          while (true) {
-            const __amdgpu_buffer_rsrc_t sr = sweep_rsrc(XB, span);
-            u32x4 vb[kSweepMode == 1 ? kSweep : 1];
-            if constexpr (kSweepMode == 1) sweep_load(vb, sr, (uint32_t)kSwCh);
-            const Desc D = describe();
-            const bool li = D.nch != 0;
-            const uint64_t a_abs = reinterpret_cast<uintptr_t>(base) + D.ao;  // first kept byte
-            const uint64_t a_end = a_abs + D.eff - 1;                         // last kept byte
-            const bool in = !li || (a_abs - XB < 16ull * span && a_end - XB < 16ull * span);
-            if (__ballot(!in) != 0) {
-              generic = true;
-              break;
-            }
-            carry_slot1 = D.carry_slot1;
-            carry_pos = D.carry_pos;
-            // range-relative chunk of the first / last kept byte (lanes without
-            // a segment: never in a window), and the byte bounds there
-            const uint32_t sc = li ? (uint32_t)((a_abs - XB) >> 4) : 0xffffffffu;
-            const uint32_t ec = li ? (uint32_t)((a_end - XB) >> 4) : 0xffffffffu;
-            const uint32_t hb = (uint32_t)a_abs & 15u;        // bytes below the first
-            const uint32_t tb = ((uint32_t)a_end & 15u) + 1u;  // bytes up to the last
-            u32x4* swd = lds_swd[wid];
-            uint32_t* swf = lds_swf[wid];
-            uint32_t seg = 0;    // F(end) - F(start), modulo 2^32
-            uint32_t fbase = 0;  // F at the window's first chunk
-            // one window: chunk sums, the prefix F, staging ...
-            auto sweep_window = [&](const u32x4 (&v)[kSweep]) {
-              uint32_t sm[kSweep], I[kSweep];
-#pragma unroll
-              for (int q = 0; q < kSweep; ++q) {
-                sm[q] = chunk_halves(v[q], 0u);  // < 2^19
-                I[q] = sm[q];
-              }
-              wave_scan_add_n<kSweep>(I);
-#pragma unroll
-              for (int q = 0; q < kSweep; ++q) {
-                swd[q * 64 + lane] = v[q];
-                swf[q * 64 + lane] = fbase + I[q] - sm[q];
-                fbase += readlane_u32(I[q], 63);
-              }
-              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            };
-            // ... then the segments whose first / last kept byte lies in it
-            auto sweep_eval = [&](uint32_t w0) {
-              const uint32_t js = sc - w0, je = ec - w0;
-              if (js < (uint32_t)kSwCh) seg -= chunk_halves_masked(swd[js], lut.m[hb], swf[js]);
-              if (je < (uint32_t)kSwCh) seg += chunk_halves_masked(swd[je], lut.m[tb], swf[je]);
-              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            };
-            bool next = false;  // the next round's first window is loading
-            uint64_t nxb = 0;
-            uint32_t nspan = 0;
-            if constexpr (kSweepMode != 1) {
-              for (uint32_t w0 = 0; w0 < span; w0 += (uint32_t)kSwCh) {
-                sweep_window(sw_va);
-                // the next window's loads fly while this one's segments are
-                // read; under the last window, the next round's first
-                if (w0 + (uint32_t)kSwCh < span) {
-                  sweep_load(sw_va, sr, w0 + (uint32_t)kSwCh);
-                } else if (kSweepMode == 2 && r0 + 64 < S1) {
-                  next = sweep_plan(so_next, l_next, nxb, nspan);
-                  if (next) sweep_load(sw_va, sweep_rsrc(nxb, nspan), 0);
-                }
-                sweep_eval(w0);
-              }
-            } else {
-              // two register sets, two windows in flight: window w + 1 is
-              // loading while window w is summed and scanned (no copy between
-              // the sets: a copy would wait for the load it copies)
-              for (uint32_t w0 = 0; w0 < span; w0 += 2u * (uint32_t)kSwCh) {
-                sweep_window(sw_va);
-                sweep_eval(w0);
-                if (w0 + (uint32_t)kSwCh >= span) break;
-                if (w0 + 2u * (uint32_t)kSwCh < span)
-                  sweep_load(sw_va, sr, w0 + 2u * (uint32_t)kSwCh);
-                sweep_window(vb);
-                sweep_eval(w0 + (uint32_t)kSwCh);
-                if (w0 + 3u * (uint32_t)kSwCh < span) sweep_load(vb, sr, w0 + 3u * (uint32_t)kSwCh);
-              }
-            }
-            if (li) atomicAdd(&acc[D.meta], (unsigned long long)seg);
-            if (!next) break;
-            // on to the next round, inside this loop
-            r0 += 64;
-            so = so_next;
-            l = l_next;
-            if (r0 + 64 < S1) fetch(r0 + 64);
-            XB = nxb;
-            span = nspan;
-          }
-          if (!generic) continue;
-        }
-      }
-      const Desc D = describe();
+      const RoundDesc D = describe_round(pkmark, lane, np, ps, r0, so, l, k_skip, k_len,
+                                         carry_slot1, carry_pos, base);
       carry_slot1 = D.carry_slot1;
       carry_pos = D.carry_pos;
       const uint32_t eff = D.eff, head = D.head, nch = D.nch, meta = D.meta;
@@ -425,38 +291,8 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
       // --- long segments: one wave-wide span each -------------------------
       const bool is_long =
           nch >= kListMax || (long_ch != 0 && nch >= long_ch);
-      for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
-        const int s = (int)__builtin_ctzll(lm);
-        // head and length read separately: a segment may hold up to 4 GiB,
-        // more than one packed 32-bit word (eff << 4 | head) keeps
-        const uint32_t h = __builtin_amdgcn_readlane(head, s);
-        const uint32_t el = __builtin_amdgcn_readlane(eff, s);
-        const uint32_t mts = __builtin_amdgcn_readlane(meta, s);
-        const uint8_t* cb = base + (readlane_u64(c0_lo, c0_hi, s));
-        const uint32_t nc = __builtin_amdgcn_readlane(nch, s);
-        // chunk k keeps bytes [k ? 0 : h, k < nc - 1 ? 16 : last_end): only the
-        // first and last chunks are partial, so no byte position is formed
-        const uint32_t last_end = ((h + (el & 15u) + 15u) & 15u) + 1u;
-        uint64_t lsum = 0;
-        for (uint32_t k0 = 0; k0 < nc; k0 += 64 * kLongU) {
-          u32x4 v[kLongU];
-#pragma unroll
-          for (int u = 0; u < kLongU; ++u)
-            if (u == 0 || k0 + 64u * u < nc)
-              v[u] = load_chunk(cb + 16ull * min(k0 + (uint32_t)(u * 64 + lane), nc - 1));
-#pragma unroll
-          for (int u = 0; u < kLongU; ++u) {
-            if (u == 0 || k0 + 64u * u < nc) {
-              const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
-              const int lo_b = k == 0 ? (int)h : (k < nc ? 0 : 16);
-              const int hi_b = k + 1 < nc ? 16 : (k + 1 == nc ? (int)last_end : 0);
-              lsum += lut.sum(v[u], lo_b, hi_b);
-            }
-          }
-        }
-        const uint32_t x = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(lsum), 0u), 63);
-        if (lane == 0) atomicAdd(&acc[mts], (unsigned long long)x);
-      }
+      stream_long(__ballot(is_long), D, base, lane, acc,
+                  [&](u32x4 v, int lo_b, int hi_b) { return lut.sum(v, lo_b, hi_b); });
       // --- the round's chunk list -----------------------------------------
       const uint32_t nch_l = is_long ? 0u : nch;
       const uint32_t ci = wave_scan<0, false>(nch_l, 0u);
@@ -552,16 +388,10 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
         if (pend) consume(va, ka);  // drain at the end of the round
         pend = 0;
       };
-#ifdef UINET_CHAINS_LAB_NOLIST  // tools/chains ablation only: descriptor rounds, no chunk list
-      (void)run;
-      if ((r16 ^ mval ^ dkr ^ (uint32_t)dk ^ (uint32_t)window ^ C) == 0x9e3779b9u)
-        atomicAdd(&acc[lane], 1ull);
-#else
       if (window)
         run(std::true_type());
       else
         run(std::false_type());
-#endif
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (lane < np) {
@@ -571,9 +401,169 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
-#ifdef UINET_CHAINS_LAB_PAD
-  if (lab_pad == 0x9e3779b9u && n == 0) out[0] = 0;  // keeps the padding live
-#endif
+}
+
+
+// k_chains_sweep: the address sweep over the rounds that qualify
+// (sweep_plan, cksum_device.h: no long segment, segments in address order
+// with no hole of 4 KiB or more, at least 4/5 of the range filled).  Two
+// windows of kSweepW passes in flight in two register sets, no copy between
+// them; when a round's last window is summed the next round's plan is made
+// from its raw descriptors (fetched a round ahead) and its first two windows
+// are issued before it is described, so a wave has loads in flight through
+// the descriptor work.  Its own resources are what set the occupancy
+// (24 KB LDS per block: 6 blocks per CU; 6 waves per SIMD), since no chunk
+// list shares the kernel.  Rounds that do not qualify take the light path:
+// long segments wave-wide, the others lane by lane with masks from a 34-entry
+// split table (fast enough for the few such rounds an ordered batch holds;
+// an unordered batch belongs to k_chains_pipe -- without the flag).
+constexpr int kSweepW = 4;
+
+template <int kTile, typename OffT, typename LenT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_chains_sweep(
+    const uint8_t* __restrict__ base, const OffT* __restrict__ seg_off,
+    const LenT* __restrict__ seg_len, const uint32_t* __restrict__ pkt_seg,
+    const uint32_t* __restrict__ plen, const uint32_t* __restrict__ pskip,
+    const uint32_t* __restrict__ seed, uint16_t* __restrict__ out, uint32_t n, uint32_t flags,
+    uint32_t long_ch) {
+  static_assert(kTile >= 1 && kTile <= 32, "see k_chains_pipe");
+  constexpr int W = kSweepW;
+  constexpr uint32_t kSwCh = 64u * W;  // chunks per window
+  __shared__ u32x4 lut_m[34];          // [e]: bytes [0, e); [17 + s]: bytes [s, 16)
+  __shared__ unsigned long long lds_acc[kWaves][2 * kTile];  // (slot, rot) bins
+  __shared__ uint32_t lds_pkmark[kWaves][64];                // packet-start markers
+  __shared__ u32x4 lds_swd[kWaves][kSwCh];                   // a window's chunks
+  __shared__ uint32_t lds_swf[kWaves][kSwCh];                // F at each chunk
+  for (int i = threadIdx.x; i < 34; i += blockDim.x)
+    lut_m[i] = i < 17 ? chunk_mask(0, i) : chunk_mask(i - 17, 16);
+  for (int i = threadIdx.x; i < kWaves * 64; i += blockDim.x) (&lds_pkmark[0][0])[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  unsigned long long* acc = lds_acc[wid];
+  uint32_t* pkmark = lds_pkmark[wid];
+  // bytes [s, e) of a chunk, as the plain sum of its 16-bit halves (< 2^19)
+  auto msum = [&](u32x4 v, int s, int e, uint32_t a) {
+    return chunk_halves_masked(v, lut_m[clampi(e, 0, 16)] & lut_m[17 + clampi(s, 0, 16)], a);
+  };
+  const uint32_t lthr = (long_ch != 0 && long_ch < kListMax) ? long_ch : kListMax;
+  const uint64_t ubase = reinterpret_cast<uintptr_t>(base);
+  const uint32_t tiles = (n + kTile - 1) / kTile;
+  const uint32_t wstride = gridDim.x * kWaves;
+
+  for (uint32_t t = blockIdx.x * kWaves + wid; t < tiles; t += wstride) {
+    const uint32_t P0 = t * kTile;
+    const int np = (int)min((uint32_t)kTile, n - P0);
+    const uint32_t ps = pkt_seg[P0 + (uint32_t)min(lane, np)];
+    const uint32_t k_skip = (lane < np && pskip) ? pskip[P0 + lane] : 0u;
+    const uint32_t k_len = (lane < np) ? (plen ? plen[P0 + lane] : 0xffffffffu) : 0u;
+    const uint32_t S0 = __builtin_amdgcn_readfirstlane(ps);
+    const uint32_t S1 = __builtin_amdgcn_readlane(ps, np);
+    if (lane < 2 * kTile) acc[lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    uint32_t carry_slot1 = 0;  // slot + 1 of the last segment of the previous round
+    uint32_t carry_pos = 0;    // chain offset just past that segment
+    uint64_t so_next = 0;
+    uint32_t l_next = 0;
+    auto fetch = [&](uint32_t r) {
+      const uint32_t s = r + (uint32_t)lane;
+      const uint32_t sc = s < S1 ? s : S1 - 1;
+      so_next = (uint64_t)seg_off[sc];
+      l_next = s < S1 ? (uint32_t)seg_len[sc] : 0u;
+    };
+    if (S0 < S1) fetch(S0);
+    u32x4 va[W], vb[W];  // the two windows in flight
+    for (uint32_t r0 = S0; r0 < S1; r0 += 64) {
+      uint64_t so = so_next;
+      uint32_t l = l_next;
+      if (r0 + 64 < S1) fetch(r0 + 64);
+      // --- rounds that qualify, back to back ------------------------------
+      uint64_t XB;
+      uint32_t span;
+      bool light = false;  // a round the plan admitted whose clipped bytes left the range
+      if (sweep_plan(ubase + so, l, lthr, XB, span)) {
+        __amdgpu_buffer_rsrc_t sr = sweep_rsrc(XB, span);
+        sweep_load<W>(va, sr, 0u, lane);
+        sweep_load<W>(vb, sr, kSwCh, lane);
+        while (true) {
+          const RoundDesc D = describe_round(pkmark, lane, np, ps, r0, so, l, k_skip, k_len,
+                                             carry_slot1, carry_pos, base);
+          const bool li = D.nch != 0;
+          const uint64_t a = ubase + D.ao;  // first kept byte
+          // clipping only shrinks a segment: its kept bytes lie in the range
+          const bool in = !li || (a - XB < 16ull * span && a + D.eff - 1 - XB < 16ull * span);
+          if (__ballot(!in) != 0) {
+            light = true;
+            break;
+          }
+          carry_slot1 = D.carry_slot1;
+          carry_pos = D.carry_pos;
+          SweepSpan<W> sp;
+          sp.init(lds_swd[wid], lds_swf[wid], lut_m, a, li ? D.eff : 0u, XB);
+          for (uint32_t w0 = 0;; w0 += 2u * kSwCh) {
+            sp.window(va, lane);
+            if (w0 + 2u * kSwCh < span) sweep_load<W>(va, sr, w0 + 2u * kSwCh, lane);
+            sp.eval(w0);
+            if (w0 + kSwCh >= span) break;
+            sp.window(vb, lane);
+            if (w0 + 3u * kSwCh < span) sweep_load<W>(vb, sr, w0 + 3u * kSwCh, lane);
+            sp.eval(w0 + kSwCh);
+            if (w0 + 2u * kSwCh >= span) break;
+          }
+          if (li) atomicAdd(&acc[D.meta], (unsigned long long)sp.seg);
+          // the next round of the tile: planned from its raw descriptors, its
+          // first two windows issued before it is described
+          if (r0 + 64 >= S1) break;
+          uint64_t nxb;
+          uint32_t nspan;
+          if (!sweep_plan(ubase + so_next, l_next, lthr, nxb, nspan)) break;
+          r0 += 64;
+          so = so_next;
+          l = l_next;
+          if (r0 + 64 < S1) fetch(r0 + 64);
+          XB = nxb;
+          span = nspan;
+          sr = sweep_rsrc(XB, span);
+          sweep_load<W>(va, sr, 0u, lane);
+          sweep_load<W>(vb, sr, kSwCh, lane);
+        }
+        if (!light) continue;
+      }
+      // --- the light path ---------------------------------------------------
+      const RoundDesc D = describe_round(pkmark, lane, np, ps, r0, so, l, k_skip, k_len,
+                                         carry_slot1, carry_pos, base);
+      carry_slot1 = D.carry_slot1;
+      carry_pos = D.carry_pos;
+      const bool is_long = D.nch >= lthr;
+      stream_long(__ballot(is_long), D, base, lane, acc,
+                  [&](u32x4 v, int lo_b, int hi_b) { return (uint64_t)msum(v, lo_b, hi_b, 0u); });
+      // the short segments lane by lane, 4 chunks in flight per lane
+      const uint32_t nch_s = is_long ? 0u : D.nch;
+      const uint32_t kmax = readlane_u32(wave_scan<1, false>(nch_s, 0u), 63);
+      const uint8_t* cb = base + D.c0;
+      const int h = (int)D.head, e = (int)(D.head + (is_long ? 0u : D.eff));
+      uint32_t sum = 0;  // < 1024 x 2^19
+      for (uint32_t k0 = 0; k0 < kmax; k0 += 4) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          v[u] = load_chunk(cb + 16ull * min(k0 + (uint32_t)u, max(nch_s, 1u) - 1u));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kb = 16 * (int)(k0 + (uint32_t)u);
+          if (k0 + (uint32_t)u < nch_s) sum = msum(v[u], h - kb, e - kb, sum);
+        }
+      }
+      if (nch_s) atomicAdd(&acc[D.meta], (unsigned long long)sum);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane < np) {
+      const uint32_t p = P0 + (uint32_t)lane;
+      const uint32_t odd = fold16(acc[2 * lane + 1]);
+      out[p] = finish(acc[2 * lane] + rot8(odd) + (seed ? seed[p] : 0u), flags);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
 }
 
 template <typename OffT, typename LenT>
@@ -593,31 +583,25 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
   blocks = blocks > cap ? cap : blocks;
   const uint32_t long_ch = (uint32_t)tn.chains_long;
-#define LF(P, T, S, M)                                                                       \
-  UINET_LAUNCH((k_chains_pipe<P, T, S, M, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0,   \
-               stream, b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
-  // chains_sweep: 0 off; 2 / 4 = windows of 2 / 4 passes; 3 = windows of 2
-  // passes, two in flight; 5 / 6 = windows of 4 / 2 passes, each round's
-  // first window issued under the previous round's last
-#define LFS(P, T)                                  \
-  do {                                             \
-    switch (tn.chains_sweep) {                     \
-      case 2: LF(P, T, 2, 0); break;               \
-      case 3: LF(P, T, 2, 1); break;               \
-      case 4: LF(P, T, 4, 0); break;               \
-      case 5: LF(P, T, 4, 2); break;               \
-      case 6: LF(P, T, 2, 2); break;               \
-      default: LF(P, T, 0, 0); break;              \
-    }                                              \
-  } while (0)
-  if (tile == 8) {
-    if (tn.chains_pass == 4) LFS(4, 8);
-    else LFS(2, 8);
-  } else {
-    if (tn.chains_pass == 4) LFS(4, 32);
-    else LFS(2, 32);
+  if (flags & UINET_CKSUM_F_ORDERED) {
+#define LS(T)                                                                                  \
+  UINET_LAUNCH((k_chains_sweep<T, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, b, \
+               seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
+    if (tile == 8) LS(8);
+    else LS(32);
+#undef LS
+    return check_launch();
   }
-#undef LFS
+#define LF(P, T)                                                                           \
+  UINET_LAUNCH((k_chains_pipe<P, T, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0,   \
+               stream, b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
+  if (tile == 8) {
+    if (tn.chains_pass == 4) LF(4, 8);
+    else LF(2, 8);
+  } else {
+    if (tn.chains_pass == 4) LF(4, 32);
+    else LF(2, 32);
+  }
 #undef LF
   return check_launch();
 }

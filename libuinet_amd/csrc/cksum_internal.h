@@ -27,7 +27,6 @@ struct Tuning {
   int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead
   int host_pin;        // host pool helpers pinned to CPUs 1.. of the process mask (0/1)
   int multi_gather;    // uinet_cksum_spans_multi: 0 RCCL gather when it applies, 1 peer copies
-  int chains_sweep;    // chain kernel: address-sweep window in 64-chunk passes (2, 4), 0 = off
 };
 Tuning tuning();
 // True when G * 16 + U names a compiled span-kernel geometry.

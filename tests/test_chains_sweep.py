@@ -1,11 +1,13 @@
-"""The chain kernel's address sweep (chains_sweep = 2 / 4): descriptor rounds
-whose list segments lie in one dense address range are read as plain chunks
-with a running prefix F, each segment summed as F(end) - F(start).  These
-layouts are built so that rounds DO qualify -- in order, shuffled inside a
-round, overlapping, 1-byte and empty segments, len/skip clipping, long
-segments inside a dense run, dense and scattered rounds mixed -- and every
-result is compared with the oracle, at every sweep window, both tile sizes,
-both batch widths and both descriptor widths.  The reference semantics are
+"""The chain kernel's address sweep (k_chains_sweep, selected by the hint
+flag UINET_CKSUM_F_ORDERED): descriptor rounds whose segments lie in one
+dense address range, in order, are read as plain chunks with a running prefix
+F, each segment summed as F(end) - F(start); other rounds take the light
+path (long segments wave-wide, the rest lane by lane).  The layouts here
+make rounds qualify (in order, overlapping, 1-byte and empty segments,
+len/skip clipping) and not qualify (shuffled inside a round, scattered
+blocks, long segments inside a dense run), and every result is compared with
+the oracle, with and without the hint, at both tile sizes, both batch widths
+of the chunk list and both descriptor widths.  The reference semantics are
 in_cksum_skip's walk (/root/reference/sys/amd64/amd64/in_cksum.c:203-229)."""
 from __future__ import annotations
 
@@ -65,7 +67,9 @@ def clip_args(rng, seg_len, pkt_seg):
     return length, skip, seed
 
 
-def run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, packed, flags=0):
+def run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, packed, flags=0,
+               ordered=True):
+    flags |= u.F_ORDERED if ordered else 0
     if packed:
         so, sl = u.pack_segments(seg_off, seg_len)
         so, sl = dev(torch, so), dev(torch, sl)
@@ -78,7 +82,7 @@ def run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, pack
 
 
 def with_knobs(knobs, fn):
-    dflt = {"chains_sweep": 2, "chains_tile": 0, "chains_pass": 2, "chains_long": 128}
+    dflt = {"chains_tile": 0, "chains_pass": 2, "chains_long": 128}
     for k, v in knobs.items():
         u.set_tuning(k, v)
     try:
@@ -89,48 +93,45 @@ def with_knobs(knobs, fn):
 
 
 @pytest.mark.parametrize("shape", ["in", "shuffled", "overlap", "mixed"])
-@pytest.mark.parametrize("sweep", [0, 2, 3, 4, 5, 6])
-def test_sweep_layouts(torch_dev, ora, shape, sweep):
+@pytest.mark.parametrize("ordered", [False, True])
+def test_sweep_layouts(torch_dev, ora, shape, ordered):
     torch = torch_dev
-    rng = np.random.default_rng(12000 + 10 * sweep + len(shape))
+    rng = np.random.default_rng(12000 + 10 * ordered + len(shape))
     arena = rand_arena(1 << 23, 120)
     seg_off, seg_len, pkt_seg = dense_layout(rng, 6000, arena.size, shape)
     length, skip, seed = clip_args(rng, seg_len, pkt_seg)
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
     for packed in (False, True):
-        got = with_knobs({"chains_sweep": sweep},
-                         lambda: run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip,
-                                            seed, packed))
+        got = run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, packed,
+                         ordered=ordered)
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("sweep", [2, 3, 4, 5, 6])
+@pytest.mark.parametrize("ordered", [False, True])
 @pytest.mark.parametrize("tile,cpass,long_ch", [(8, 2, 128), (32, 4, 128), (32, 2, 16), (8, 4, 0)])
-def test_sweep_geometries(torch_dev, ora, sweep, tile, cpass, long_ch):
+def test_sweep_geometries(torch_dev, ora, ordered, tile, cpass, long_ch):
     """Dense rounds at both tile sizes and batch widths, with long segments
     (streamed wave-wide, outside the sweep) inside the dense run."""
     torch = torch_dev
-    rng = np.random.default_rng(13000 + sweep + tile + cpass + long_ch)
+    rng = np.random.default_rng(13000 + ordered + tile + cpass + long_ch)
     arena = rand_arena(1 << 23, 130)
     seg_off, seg_len, pkt_seg = dense_layout(rng, 3000, arena.size, "in", max_seg=600)
     length, skip, seed = clip_args(rng, seg_len, pkt_seg)
     for flags in (0, u.F_UDP):
         want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed,
                           flags=flags)
-        got = with_knobs({"chains_sweep": sweep, "chains_tile": tile, "chains_pass": cpass,
-                          "chains_long": long_ch},
+        got = with_knobs({"chains_tile": tile, "chains_pass": cpass, "chains_long": long_ch},
                          lambda: run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip,
-                                            seed, False, flags))
+                                            seed, False, flags, ordered))
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("sweep", [2, 3, 4, 5, 6])
-def test_sweep_extremes(torch_dev, ora, sweep):
+def test_sweep_extremes(torch_dev, ora):
     """All-0x00 and all-0xff bytes (0 vs 0xffff after the fold), rounds of 64
     one-byte segments, segments ending on the arena's last byte, and rounds
     whose list runs 1023 chunks (the longest the chunk list takes)."""
     torch = torch_dev
-    rng = np.random.default_rng(14000 + sweep)
+    rng = np.random.default_rng(14000)
     for fill in (0x00, 0xFF):
         arena = aligned_empty(1 << 22)
         arena[:] = fill
@@ -138,9 +139,7 @@ def test_sweep_extremes(torch_dev, ora, sweep):
         length, skip, seed = clip_args(rng, seg_len, pkt_seg)
         seed[:] = 0
         want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
-        got = with_knobs({"chains_sweep": sweep},
-                         lambda: run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip,
-                                            seed, False))
+        got = run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, False)
         np.testing.assert_array_equal(got, want)
     arena = rand_arena(1 << 24, 140)
     n = 400
@@ -156,14 +155,14 @@ def test_sweep_extremes(torch_dev, ora, sweep):
     length, skip, seed = clip_args(rng, seg_len, pkt_seg)
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
     for tile in (8, 32):
-        got = with_knobs({"chains_sweep": sweep, "chains_tile": tile, "chains_long": 0},
+        got = with_knobs({"chains_tile": tile, "chains_long": 0},
                          lambda: run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip,
                                             seed, False))
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("sweep", [0, 2, 3, 4, 5, 6])
-def test_sweep_config3_slice(torch_dev, ora, sweep):
+@pytest.mark.parametrize("ordered", [False, True])
+def test_sweep_config3_slice(torch_dev, ora, ordered):
     """Config 3's own layout (m_fragment chains, in order, 0-7-B gaps) at
     65,536 packets, wide and packed descriptors."""
     torch = torch_dev
@@ -175,13 +174,10 @@ def test_sweep_config3_slice(torch_dev, ora, sweep):
                       length=lay["lens"], skip=np.full(c["n"], 20, np.int64))
     packed = u.pack_segments(c["seg_off"], c["seg_len"])
 
-    def go():
-        a = host16(u.cksum_chains(c["arena"], c["seg_off"], c["seg_len"], c["pkt_seg"],
-                                  length=c["len"], skip=c["skip"], len_hint=c["mean_seg"]))
-        b = host16(u.cksum_chains(c["arena"], packed[0], packed[1], c["pkt_seg"],
-                                  length=c["len"], skip=c["skip"], len_hint=c["mean_seg"]))
-        return a, b
-
-    a, b = with_knobs({"chains_sweep": sweep}, go)
+    fl = u.F_ORDERED if ordered else 0
+    a = host16(u.cksum_chains(c["arena"], c["seg_off"], c["seg_len"], c["pkt_seg"],
+                              length=c["len"], skip=c["skip"], flags=fl, len_hint=c["mean_seg"]))
+    b = host16(u.cksum_chains(c["arena"], packed[0], packed[1], c["pkt_seg"],
+                              length=c["len"], skip=c["skip"], flags=fl, len_hint=c["mean_seg"]))
     np.testing.assert_array_equal(a, want)
     np.testing.assert_array_equal(b, want)
