@@ -58,10 +58,6 @@ def parse():
     ap.add_argument("--desc", choices=["wide", "packed"], default="wide",
                     help="12-B wide (uinet_cksum_chains / uinet_cksum_spans) or packed "
                     "6-B (uinet_cksum_chains32 / uinet_cksum_spans32) descriptors")
-    ap.add_argument("--ordered", choices=["auto", "on", "off"], default="auto",
-                    help="chain configs: pass UINET_CKSUM_F_ORDERED (segments mostly in "
-                    "address order: the chain kernel's address sweep); auto = on for config 3, "
-                    "whose m_fragment segments are laid out in order, off for 3tx / 5tso")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
@@ -159,14 +155,6 @@ def build_workload(cfg: str, n, rank: int, world: int = 1):
                      f"src,dst,TCP/UDP)")
         w["hint"] = 8980
     return w
-
-
-def chain_flags(cfg: str, ordered: str = "auto") -> int:
-    """The hint flags a chain config's launch passes (bench --ordered)."""
-    import libuinet_amd as u
-
-    on = cfg == "3" if ordered == "auto" else ordered == "on"
-    return u.F_ORDERED if on else 0
 
 
 def make_launch(cfg: str, w, api: str, out, desc: str = "wide", flags: int = 0):
@@ -551,8 +539,7 @@ def run(args, distributed: bool, wd):
         w["packed"] = u.pack_segments(w["seg_off"], w["seg_len"])
     elif args.desc == "packed" and args.api == "spans":
         w["packed"] = u.pack_segments(w["off"], w["len"])
-    cflags = chain_flags(args.config, args.ordered) if args.config in CHAIN_CONFIGS else 0
-    launches = [make_launch(args.config, w, args.api, o, args.desc, cflags) for o in outs]
+    launches = [make_launch(args.config, w, args.api, o, args.desc) for o in outs]
     counts = [n] * world
     rg = ResultGather(counts, "cuda", depth=NBUF) if distributed else None
     K, Wm = args.steps, args.warmup
@@ -649,8 +636,7 @@ def run(args, distributed: bool, wd):
                 "api": {"spans": "uinet_cksum_spans" + ("32" if args.desc == "packed" else ""),
                         "strided": "uinet_cksum_strided"}[args.api]
                 if args.config not in CHAIN_CONFIGS else
-                {"wide": "uinet_cksum_chains", "packed": "uinet_cksum_chains32"}[args.desc]
-                + (" + UINET_CKSUM_F_ORDERED" if cflags else ""),
+                {"wide": "uinet_cksum_chains", "packed": "uinet_cksum_chains32"}[args.desc],
                 "parallelism": f"dp{world} packet shards" + (
                     f" + {'RCCL' if backend == 'nccl' else backend} gather of u16 results, "
                     "overlapped with the next step's kernel" if distributed else ""),

@@ -131,13 +131,6 @@ int in6_cksum_pseudo(struct ip6_hdr *ip6, uint32_t len, uint8_t nxt,
 /* Result flags for the batch/device entry points. */
 #define UINET_CKSUM_F_UDP           0x1u /* 0 -> 0xffff (ip_output.c:962-963) */
 #define UINET_CKSUM_F_NO_COMPLEMENT 0x2u /* return the folded sum, in_pseudo-style */
-/* A performance hint for uinet_cksum_chains / uinet_cksum_chains32 (never
- * changes results): the batch's segments lie mostly in address order, close
- * together -- mbufs carved one after another out of large buffers.  The
- * chain kernel then reads such runs of segments as plain 16-B chunks (the
- * address sweep) and checks every 64-segment round before it does; a round
- * that is not ordered takes a slower path, so a wrong hint costs time only. */
-#define UINET_CKSUM_F_ORDERED       0x4u
 
 /* Engine version string and HIP diagnostics. */
 const char *uinet_cksum_version(void);

@@ -29,7 +29,7 @@ __all__ = [
     "LIB_PATH", "CksumError", "lib", "in_cksum", "in_cksum_skip", "in_cksum_pseudo_header",
     "in_cksum_hdr", "in_pseudo", "in_addword", "in_cksum_skip_batch",
     "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch", "cksum_spans", "cksum_strided",
-    "cksum_chains", "pack_segments", "F_UDP", "F_NO_COMPLEMENT", "F_ORDERED", "MbufChains", "MBUF_DTYPE", "MSIZE",
+    "cksum_chains", "pack_segments", "F_UDP", "F_NO_COMPLEMENT", "MbufChains", "MBUF_DTYPE", "MSIZE",
     "SEED_BASE", "aligned_empty", "splitmix64_bytes", "EXPORTED_SYMBOLS", "cksum_spans_multi",
     "in_cksum_skip_batch_multi",
 ]
@@ -38,7 +38,6 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libuinet_ck
 
 F_UDP = 0x1
 F_NO_COMPLEMENT = 0x2
-F_ORDERED = 0x4  # chains: segments mostly in address order (a hint; results unchanged)
 
 OK, EINVAL, ENODEV, ENOMEM, EHIP = 0, -22, -19, -12, -5
 

@@ -326,117 +326,4 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
 }
 
-// Lane i gets lane i-1's x (DPP wave_shr:1; lane 0 gets 0).  Needs all 64
-// lanes active.
-__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, true);
-}
-
-// ---- The address sweep ---------------------------------------------------------
-// A wave whose spans (chain segments, small packets) lie in one dense address
-// range reads that range as plain 16-B chunks, W passes of 64 per window, with
-// no per-chunk span lookup, mask or bin.  Each chunk adds its whole
-// 8-halfword sum to a running prefix F (one DPP scan per pass); F and the
-// chunk are staged in LDS for the window, and each span's lane reads, in the
-// window holding its first and its last byte,
-//   F(x) = F(first byte of x's chunk) + (halves of x's chunk below x)
-// so the span's sum is F(end) - F(start): exact modulo 2^32 for a span of
-// under 16 KiB (weighted sum < 2^29).  Used by the chain kernel
-// (cksum_chains.hip) and by k_spans_quad for dense small packets.
-
-// One span per lane, [a0, a0 + l) (absolute address; l = 0: none).  True, with
-// the range's first chunk XB (a byte address) and its length in chunks, when
-// the spans, in lane order, start at non-decreasing addresses, leave no hole
-// of 4 KiB or more between them (every byte the sweep reads then shares a
-// 4-KiB page with a span byte: nothing unmapped is touched), each touch fewer
-// than lthr (<= 1024) chunks, and fill at least 4/5 of the range.  All 64
-// lanes must be active.
-__device__ __forceinline__ bool sweep_plan(uint64_t a0, uint32_t l, uint32_t lthr, uint64_t& XB,
-                                           uint32_t& span) {
-  const uint32_t rnch = l ? (uint32_t)(((a0 + l - 1) >> 4) - (a0 >> 4)) + 1u : 0u;
-  const bool el = l != 0;
-  const uint64_t em = __ballot(el);
-  if (em == 0 || __ballot(rnch >= lthr) != 0) return false;
-  const int fl = (int)__builtin_ctzll(em);
-  XB = readlane_u64((uint32_t)a0, (uint32_t)(a0 >> 32), fl) & ~15ull;
-  const uint64_t d = a0 - XB;  // huge when below XB: fails the order test
-  const bool near = d < (1ull << 30);
-  const uint32_t rs = el ? (uint32_t)d : 0u;
-  const uint32_t re = el ? rs + l : 0u;
-  const uint32_t ms = wave_scan<1, false>(rs, 0u);  // max start so far
-  const uint32_t me = wave_scan<1, false>(re, 0u);  // max end so far
-  const uint32_t ms_prev = wave_shr1(ms), me_prev = wave_shr1(me);
-  const bool bad = el && (!near || rs < ms_prev || (rs > me_prev && rs - me_prev >= 4096u));
-  const uint32_t C0 = readlane_u32(wave_scan<0, false>(rnch, 0u), 63);
-  span = ((readlane_u32(me, 63) - 1u) >> 4) + 1u;
-  return __ballot(bad) == 0 && span <= C0 + (C0 >> 2) + 64u;
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sweep_rsrc(uint64_t XB, uint32_t span) {
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(XB), 0, (int)(16u * span),
-                                           0x00020000);
-}
-
-// Window w0's chunks (non-temporal).  Chunks past the range read 0 (buffer
-// range check): no clamp, no fault, no memory traffic -- so the loads are
-// issued unconditionally.
-template <int W>
-__device__ __forceinline__ void sweep_load(u32x4 (&v)[W], __amdgpu_buffer_rsrc_t sr, uint32_t w0,
-                                           uint32_t lane) {
-#pragma unroll
-  for (int q = 0; q < W; ++q)
-    v[q] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(16u * (w0 + (uint32_t)q * 64u + lane)),
-                                                 0, 2);
-}
-
-// One lane's span over a range: F(end) - F(start) accumulated window by
-// window.  `swd` / `swf`: the wave's LDS staging (64 W chunks, 64 W words);
-// `below[k]`: the mask keeping bytes [0, k) of a chunk (k = 0..16).
-template <int W>
-struct SweepSpan {
-  u32x4* swd;
-  uint32_t* swf;
-  const u32x4* below;
-  uint32_t sc, ec, hb, tb;  // range chunk of the first / last byte, bytes below / up to them
-  uint32_t seg, fbase;
-
-  __device__ __forceinline__ void init(u32x4* d, uint32_t* f, const u32x4* m, uint64_t a,
-                                       uint32_t len, uint64_t XB) {
-    swd = d;
-    swf = f;
-    below = m;
-    const uint64_t e = a + len - 1;
-    sc = len ? (uint32_t)((a - XB) >> 4) : 0xffffffffu;  // no span: never in a window
-    ec = len ? (uint32_t)((e - XB) >> 4) : 0xffffffffu;
-    hb = (uint32_t)a & 15u;
-    tb = ((uint32_t)e & 15u) + 1u;
-    seg = 0;
-    fbase = 0;
-  }
-  // the window's chunk sums, prefix F and staging
-  __device__ __forceinline__ void window(const u32x4 (&v)[W], uint32_t lane) {
-    uint32_t sm[W], I[W];
-#pragma unroll
-    for (int q = 0; q < W; ++q) {
-      sm[q] = chunk_halves(v[q], 0u);  // < 2^19
-      I[q] = sm[q];
-    }
-    wave_scan_add_n<W>(I);
-#pragma unroll
-    for (int q = 0; q < W; ++q) {
-      swd[q * 64 + lane] = v[q];
-      swf[q * 64 + lane] = fbase + I[q] - sm[q];
-      fbase += readlane_u32(I[q], 63);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
-  // the span's first / last byte when it lies in the window at chunk w0
-  __device__ __forceinline__ void eval(uint32_t w0) {
-    const uint32_t js = sc - w0, je = ec - w0;
-    if (js < 64u * W) seg -= chunk_halves_masked(swd[js], below[hb], swf[js]);
-    if (je < 64u * W) seg += chunk_halves_masked(swd[je], below[tb], swf[je]);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
-};
-
 }  // namespace uinet

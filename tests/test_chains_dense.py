@@ -1,14 +1,12 @@
-"""The chain kernel's address sweep (k_chains_sweep, selected by the hint
-flag UINET_CKSUM_F_ORDERED): descriptor rounds whose segments lie in one
-dense address range, in order, are read as plain chunks with a running prefix
-F, each segment summed as F(end) - F(start); other rounds take the light
-path (long segments wave-wide, the rest lane by lane).  The layouts here
-make rounds qualify (in order, overlapping, 1-byte and empty segments,
-len/skip clipping) and not qualify (shuffled inside a round, scattered
-blocks, long segments inside a dense run), and every result is compared with
-the oracle, with and without the hint, at both tile sizes, both batch widths
-of the chunk list and both descriptor widths.  The reference semantics are
-in_cksum_skip's walk (/root/reference/sys/amd64/amd64/in_cksum.c:203-229)."""
+"""Chain batches whose segments are carved densely out of the arena -- in
+order, shuffled inside a round, overlapping, scattered blocks between them,
+1-byte and empty segments, len/skip clipping, long segments inside a dense
+run, rounds whose chunk list runs 1,023 chunks, segments ending on the
+arena's last byte, all-0x00 / all-0xff bytes -- through the chain kernel at
+both tile sizes, both batch widths and both descriptor widths, against the
+oracle's in_cksum_skip walk (/root/reference/sys/amd64/amd64/in_cksum.c
+:203-229).  (Round 4 measured an address-sweep formulation on these layouts
+and removed it, profiles/r04/pruned/; the layouts stay as parity cases.)"""
 from __future__ import annotations
 
 import numpy as np
@@ -67,9 +65,7 @@ def clip_args(rng, seg_len, pkt_seg):
     return length, skip, seed
 
 
-def run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, packed, flags=0,
-               ordered=True):
-    flags |= u.F_ORDERED if ordered else 0
+def run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, packed, flags=0):
     if packed:
         so, sl = u.pack_segments(seg_off, seg_len)
         so, sl = dev(torch, so), dev(torch, sl)
@@ -93,27 +89,24 @@ def with_knobs(knobs, fn):
 
 
 @pytest.mark.parametrize("shape", ["in", "shuffled", "overlap", "mixed"])
-@pytest.mark.parametrize("ordered", [False, True])
-def test_sweep_layouts(torch_dev, ora, shape, ordered):
+def test_dense_layouts(torch_dev, ora, shape):
     torch = torch_dev
-    rng = np.random.default_rng(12000 + 10 * ordered + len(shape))
+    rng = np.random.default_rng(12000 + len(shape))
     arena = rand_arena(1 << 23, 120)
     seg_off, seg_len, pkt_seg = dense_layout(rng, 6000, arena.size, shape)
     length, skip, seed = clip_args(rng, seg_len, pkt_seg)
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
     for packed in (False, True):
-        got = run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, packed,
-                         ordered=ordered)
+        got = run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, packed)
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("ordered", [False, True])
 @pytest.mark.parametrize("tile,cpass,long_ch", [(8, 2, 128), (32, 4, 128), (32, 2, 16), (8, 4, 0)])
-def test_sweep_geometries(torch_dev, ora, ordered, tile, cpass, long_ch):
+def test_dense_geometries(torch_dev, ora, tile, cpass, long_ch):
     """Dense rounds at both tile sizes and batch widths, with long segments
-    (streamed wave-wide, outside the sweep) inside the dense run."""
+    (streamed wave-wide) inside the dense run."""
     torch = torch_dev
-    rng = np.random.default_rng(13000 + ordered + tile + cpass + long_ch)
+    rng = np.random.default_rng(13000 + tile + cpass + long_ch)
     arena = rand_arena(1 << 23, 130)
     seg_off, seg_len, pkt_seg = dense_layout(rng, 3000, arena.size, "in", max_seg=600)
     length, skip, seed = clip_args(rng, seg_len, pkt_seg)
@@ -122,11 +115,11 @@ def test_sweep_geometries(torch_dev, ora, ordered, tile, cpass, long_ch):
                           flags=flags)
         got = with_knobs({"chains_tile": tile, "chains_pass": cpass, "chains_long": long_ch},
                          lambda: run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip,
-                                            seed, False, flags, ordered))
+                                            seed, False, flags))
         np.testing.assert_array_equal(got, want)
 
 
-def test_sweep_extremes(torch_dev, ora):
+def test_dense_extremes(torch_dev, ora):
     """All-0x00 and all-0xff bytes (0 vs 0xffff after the fold), rounds of 64
     one-byte segments, segments ending on the arena's last byte, and rounds
     whose list runs 1023 chunks (the longest the chunk list takes)."""
@@ -161,8 +154,7 @@ def test_sweep_extremes(torch_dev, ora):
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("ordered", [False, True])
-def test_sweep_config3_slice(torch_dev, ora, ordered):
+def test_config3_slice(torch_dev, ora):
     """Config 3's own layout (m_fragment chains, in order, 0-7-B gaps) at
     65,536 packets, wide and packed descriptors."""
     torch = torch_dev
@@ -174,7 +166,7 @@ def test_sweep_config3_slice(torch_dev, ora, ordered):
                       length=lay["lens"], skip=np.full(c["n"], 20, np.int64))
     packed = u.pack_segments(c["seg_off"], c["seg_len"])
 
-    fl = u.F_ORDERED if ordered else 0
+    fl = 0
     a = host16(u.cksum_chains(c["arena"], c["seg_off"], c["seg_len"], c["pkt_seg"],
                               length=c["len"], skip=c["skip"], flags=fl, len_hint=c["mean_seg"]))
     b = host16(u.cksum_chains(c["arena"], packed[0], packed[1], c["pkt_seg"],

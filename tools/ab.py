@@ -6,9 +6,7 @@ device-to-device spread hit every variant alike).
 
 Each variant is a comma list of key=value pairs for uinet_cksum_set_tuning;
 the pseudo-key desc=1 launches with packed descriptors (uinet_cksum_spans32 /
-uinet_cksum_chains32) instead of wide ones (desc=0, the default), and
-ordered=1 / 0 passes UINET_CKSUM_F_ORDERED to a chain launch or not (default
-as bench.py --ordered auto).
+uinet_cksum_chains32) instead of wide ones (desc=0, the default).
 Prints one JSON object: per variant the median / min kernel ms and GB/s.
 """
 from __future__ import annotations
@@ -50,16 +48,8 @@ def main():
         w["packed"] = u.pack_segments(w["seg_off"], w["seg_len"])
     elif a.api == "spans":
         w["packed"] = u.pack_segments(w["off"], w["len"])
-    chain = a.config in bench.CHAIN_CONFIGS
-    dflt_ord = int(bench.chain_flags(a.config) != 0) if chain else 0
-    launches = {}
-    for d in (0, 1):
-        for o in (0, 1):
-            if (d and "packed" not in w) or (o and not chain):
-                continue
-            launches[(d, o)] = bench.make_launch(a.config, w, a.api, out, "packed" if d else "wide",
-                                                 bench.chain_flags(a.config, "on" if o else "off")
-                                                 if chain else 0)
+    launches = {0: bench.make_launch(a.config, w, a.api, out),
+                1: bench.make_launch(a.config, w, a.api, out, "packed") if "packed" in w else None}
     variants = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(",") if kv)
                 for v in a.variants]
     # Every key any variant names goes back to its default before each variant
@@ -67,9 +57,9 @@ def main():
     # had set, so e.g. "spans_pipe=1" after "blocks_per_cu=4096" ran at 4096.)
     for v in variants:
         for k in v:
-            if k in ("desc", "ordered"):
-                if (v.get("desc", 0), v.get("ordered", dflt_ord)) not in launches:
-                    raise SystemExit(f"tools/ab.py: {k}={v[k]} does not apply here")
+            if k == "desc":
+                if launches.get(v[k]) is None:
+                    raise SystemExit(f"tools/ab.py: desc={v[k]} does not apply here")
                 continue
             if k not in DEFAULTS:
                 raise SystemExit(f"tools/ab.py: no default recorded for knob {k!r}")
@@ -77,12 +67,12 @@ def main():
     ref = None
     for r in range(a.rounds):
         for i, v in enumerate(variants):
-            for k in {k for vv in variants for k in vv} - {"desc", "ordered"}:
+            for k in {k for vv in variants for k in vv} - {"desc"}:
                 u.set_tuning(k, DEFAULTS[k])
             for k, val in v.items():
-                if k not in ("desc", "ordered"):
+                if k != "desc":
                     u.set_tuning(k, val)
-            launch = launches[(v.get("desc", 0), v.get("ordered", dflt_ord))]
+            launch = launches[v.get("desc", 0)]
             launch(s)  # warm
             torch.cuda.synchronize()
             if ref is None:

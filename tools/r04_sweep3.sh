@@ -3,7 +3,7 @@
 # against k_chains_pipe: chain GPU parity and smoke, interleaved A/B per chain
 # config, SQ counters of both kernels on config 3.
 set -u
-TAG=${TAG:-r04c}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+TAG=${TAG:-r04d}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 timeout -k 10 600 python -u -m pytest tests/test_chains_sweep.py tests/test_chains32.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_sweep.log 2>&1
 rc=$?; tail -n 1 $OUT/pytest_sweep.log; [ $rc -eq 0 ] || { echo FATAL $rc; exit $rc; }
