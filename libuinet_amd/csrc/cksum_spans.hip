@@ -76,6 +76,12 @@ constexpr SplitWords make_split_words() {
 __device__ const SplitWords g_split_words = make_split_words();
 
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// A compiler-only memory barrier placed right after a batch of loads: the
+// loads stay where they are issued.  Without it the compiler sinks a step's
+// loads past the previous step's sum whenever that sum has a loop of its own
+// (G = 64: spans longer than one round), which drains the pipeline there.
+// No instruction is emitted and no wait: the barrier names no registers.
+__device__ __forceinline__ void issued() { asm volatile("" ::: "memory"); }
 // A wave-uniform value the compiler may not reason about (keeps 32-bit
 // compares of a 64-bit value's halves from being merged back into a 64-bit
 // compare, which only the vector ALU has).
@@ -303,6 +309,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
   auto load_step = [&](const Step<kP>& s, u32x4 (&v)[kU]) {
     Geo<kP> z;
     load_round(addr(s, z), 0, v);
+    issued();
     return z;
   };
 
@@ -373,20 +380,22 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
         acc = fold16_32(acc) + r;  // < 2^21: 64 lanes of it still fit 32 bits
       };
       if constexpr (kP == 1) {
-        // one packet per wave (9000-B frames: three 3-KB rounds): round i + 1
-        // loads while round i is summed, two register sets in turn; a round
-        // past the end re-reads the span's last chunk (never loaded under a
-        // branch, so the wait for round i leaves round i + 1 in flight)
-        const uint32_t nr = (emax - 1) / kRound;  // rounds after round 0, >= 1
+        // one packet per wave (9000-B frames: three 3-KB rounds).  Rounds 1
+        // and 2 are straight-line code with both rounds' loads issued before
+        // the first sum (a span of one round more re-reads its last chunk in
+        // round 2, masked away); spans longer than three rounds finish
+        // serially.  (The ping-pong loop this replaces ran its rounds
+        // serially: the compiler waited for all loads where the loop's paths
+        // met, draining the pipeline at every round.)
         u32x4 x[kU], y[kU];
         load_round(w, kRound, x);
-        for (uint32_t i = 1;; i += 2) {
-          load_round(w, (i + 1) * kRound, y);
-          round_sum(x, i * kRound);
-          if (i + 1 > nr) break;
-          load_round(w, (i + 2) * kRound, x);
-          round_sum(y, (i + 1) * kRound);
-          if (i + 2 > nr) break;
+        load_round(w, 2 * kRound, y);
+        issued();
+        round_sum(x, kRound);
+        round_sum(y, 2 * kRound);
+        for (uint32_t rb = 3 * kRound; rb < emax; rb += kRound) {
+          load_round(w, rb, x);
+          round_sum(x, rb);
         }
       } else {
         for (uint32_t rb = kRound; rb < emax; rb += kRound) {
