@@ -161,7 +161,7 @@ int uinet_cksum_device_ok(void);
  *                     at 4); 0 = one packet per lane group, one-shot grid
  *   "spans_geo"       span kernels: force the lanes-per-packet G and loads
  *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
- *                     16x3, 32x3, 64x2, 64x3); 0 = picked from len_hint
+ *                     16x3, 32x3, 64x2, 64x3, 64x9); 0 = picked from len_hint
  *   "walk_prefetch"   host-mbuf batch walk: 0 = no prefetch, 1 = prefetch
  *                     mbuf headers a few packets ahead (default)
  *   "host_pin"        host pool helpers pinned to CPUs of the process mask

@@ -64,7 +64,7 @@ int launch_spans32(const void* base, const uint32_t* off, const uint16_t* len,
 template <typename OffT, typename LenT>
 int launch_spans_lean(const void* base, const OffT* off, const LenT* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
-                      uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
+                      uint32_t flags, int g, int u, bool strided, uint64_t stride, uint32_t slen,
                       int blocks_cu, hipStream_t stream);
 // k_spans_quad (cksum_spans.hip): 4 lanes per packet, U = 1 or 2 chunk
 // slots per lane, for small packets.  Same instantiations.

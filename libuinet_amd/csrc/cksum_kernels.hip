@@ -180,6 +180,9 @@ Geometry pick_geometry(uint32_t mean_len) {
   if (mean_len <= 224) return {8, 2};
   if (mean_len <= 720) return {16, 3};
   if (mean_len <= 1520) return {32, 3};
+  // 64 lanes x 9 loads: a 9000-B frame in one round, two frames in flight per
+  // wave (config 5 +2.6 % over three 3-KB rounds, profiles/r04/r04c5u9/)
+  if (mean_len > 6144) return {64, 9};
   return {64, 3};
 }
 
@@ -213,7 +216,7 @@ int grid_for(uint32_t n, int g, int bpc) {
 bool span_geometry_ok(int code) {
   switch (code) {
     case 4 * 16 + 1: case 4 * 16 + 2: case 8 * 16 + 1: case 8 * 16 + 2: case 16 * 16 + 3:
-    case 32 * 16 + 3: case 64 * 16 + 2: case 64 * 16 + 3:
+    case 32 * 16 + 3: case 64 * 16 + 2: case 64 * 16 + 3: case 64 * 16 + 9:
       return true;
     default:
       return false;
@@ -263,9 +266,9 @@ static int launch_spans_t(const void* base, const OffT* off, const LenT* len,
     return launch_spans_quad(base, off, len, seed, parity, out, n, flags, geo.u, false, 0, 0,
                              blocks_per_cu(128), stream);
   const bool sdesc = geo.g >= 32;
-  if (sdesc && pipe == 1 && geo.u == 3)
-    return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, false, 0, 0,
-                             tuning().blocks_per_cu, stream);
+  if (sdesc && pipe == 1 && (geo.u == 3 || geo.u == 9))
+    return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, geo.u, false, 0,
+                             0, tuning().blocks_per_cu, stream);
   const int grid = grid_for(n, geo.g, sdesc ? 512 : 256);
 #define L(G, U)                                                                          \
   if (sdesc && (G) >= 32)                                                                \
@@ -316,9 +319,9 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
     return launch_spans_quad<uint64_t, uint32_t>(base, nullptr, nullptr, seed, nullptr, out, n,
                                                  flags, 1, true, pkt_stride, len,
                                                  blocks_per_cu(128), stream);
-  if (geo.g >= 32 && pipe == 1 && geo.u == 3)
+  if (geo.g >= 32 && pipe == 1 && (geo.u == 3 || geo.u == 9))
     return launch_spans_lean<uint64_t, uint32_t>(base, nullptr, nullptr, seed, nullptr, out, n,
-                                                 flags, geo.g, true, pkt_stride, len,
+                                                 flags, geo.g, geo.u, true, pkt_stride, len,
                                                  tuning().blocks_per_cu, stream);
   // one packet per group suits long packets; small ones want groups that
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)

@@ -49,8 +49,6 @@
 namespace uinet {
 namespace {
 
-constexpr int kU = 3;  // chunk loads per lane and packet in one round
-
 // The chunk masks as two 17-entry rows, a constant image that a block copies
 // into LDS (instead of computing ~30 VALU per entry): entry e keeps bytes
 // [0, e) of a 16-byte chunk, entry 17 + s keeps bytes [s, 16); the mask of
@@ -153,13 +151,15 @@ struct Geo {
   uint32_t sd[kP];  // Step::sd
 };
 
-template <int G, bool kParity, bool kSeed, bool kStrided, typename OffT, typename LenT>
+template <int G, int kU, bool kParity, bool kSeed, bool kStrided, typename OffT, typename LenT>
 __global__ __launch_bounds__(kBlock) void k_spans_lean(
     const uint8_t* __restrict__ base, const OffT* __restrict__ off,
     const LenT* __restrict__ len, const uint32_t* __restrict__ seed,
     const uint8_t* __restrict__ parity, uint16_t* __restrict__ out, uint32_t n, uint32_t flags,
     uint32_t remap, uint64_t stride, uint32_t slen) {
   static_assert(G == 32 || G == 64, "one or two packets per wave");
+  static_assert(kU == 3 || (G == 64 && kU == 9), "chunk loads per lane and round: 3, or 9 at 64 "
+                                                 "lanes (a 9000-B frame in one round)");
   constexpr int kP = 64 / G;
   constexpr uint32_t kGroups = kBlock / G;
   constexpr uint32_t kRound = 16u * G * kU;  // bytes of a span one round covers
@@ -379,8 +379,9 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
           r = dot_acc_masked(x[u], lut_m[clampi((int)(e0 - rb - 16u * u * G), 0, 16)], r);
         acc = fold16_32(acc) + r;  // < 2^21: 64 lanes of it still fit 32 bits
       };
-      if constexpr (kP == 1) {
-        // one packet per wave (9000-B frames: three 3-KB rounds).  Rounds 1
+      if constexpr (kP == 1 && kU <= 3) {
+        // one packet per wave, 3-KB rounds (spans of 1.5-6 KB mean length, or
+        // of unknown length; 9000-B frames take kU = 9, one round).  Rounds 1
         // and 2 are straight-line code with both rounds' loads issued before
         // the first sum (a span of one round more re-reads its last chunk in
         // round 2, masked away); spans longer than three rounds finish
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
           load_round(w, rb, x);
           round_sum(x, rb);
         }
-      } else {
+      } else {  // two packets per wave, or 9-KB rounds: one round at a time
         for (uint32_t rb = kRound; rb < emax; rb += kRound) {
           u32x4 x[kU];
           load_round(w, rb, x);
@@ -945,8 +946,8 @@ int launch_spans_quad(const void* base, const OffT* off, const LenT* len,
 template <typename OffT, typename LenT>
 int launch_spans_lean(const void* base, const OffT* off, const LenT* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
-                      uint32_t flags, int g, bool strided, uint64_t stride, uint32_t slen,
-                      int blocks_cu, hipStream_t stream) {
+                      uint32_t flags, int g, int u, bool strided, uint64_t stride,
+                      uint32_t slen, int blocks_cu, hipStream_t stream) {
   const uint32_t groups = kBlock / g;
   // Two steps per wave by default at 32 lanes per packet (2 x 1500 B each):
   // config 2 at 2 steps (256 blocks per CU) is flat through the driver's
@@ -966,26 +967,28 @@ int launch_spans_lean(const void* base, const OffT* off, const LenT* len,
   const uint8_t* b = static_cast<const uint8_t*>(base);
   const uint32_t remap = (uint32_t)tuning().xcd_remap;
   constexpr bool kWide = sizeof(OffT) == 8;
-#define UINET_LEAN(G, P, SD, ST)                                                              \
-  UINET_LAUNCH((k_spans_lean<G, P, SD, ST, OffT, LenT>), grid, blk, 0, stream, b, off, \
-                     len, seed, parity, out, n, flags, remap, stride, slen)
-#define UINET_LEAN_G(G)                                          \
+#define UINET_LEAN(G, U, P, SD, ST)                                                   \
+  UINET_LAUNCH((k_spans_lean<G, U, P, SD, ST, OffT, LenT>), grid, blk, 0, stream, b, off, \
+               len, seed, parity, out, n, flags, remap, stride, slen)
+#define UINET_LEAN_G(G, U)                                       \
   if (strided) { /* wide descriptors only: none are read */     \
     if constexpr (kWide) {                                       \
-      if (seed) UINET_LEAN(G, false, true, true);                \
-      else UINET_LEAN(G, false, false, true);                    \
+      if (seed) UINET_LEAN(G, U, false, true, true);             \
+      else UINET_LEAN(G, U, false, false, true);                 \
     }                                                            \
   } else if (parity) {                                           \
-    if (seed) UINET_LEAN(G, true, true, false);                  \
-    else UINET_LEAN(G, true, false, false);                      \
+    if (seed) UINET_LEAN(G, U, true, true, false);               \
+    else UINET_LEAN(G, U, true, false, false);                   \
   } else {                                                       \
-    if (seed) UINET_LEAN(G, false, true, false);                 \
-    else UINET_LEAN(G, false, false, false);                     \
+    if (seed) UINET_LEAN(G, U, false, true, false);              \
+    else UINET_LEAN(G, U, false, false, false);                  \
   }
   if (g == 32) {
-    UINET_LEAN_G(32)
+    UINET_LEAN_G(32, 3)
+  } else if (u == 9) {
+    UINET_LEAN_G(64, 9)
   } else {
-    UINET_LEAN_G(64)
+    UINET_LEAN_G(64, 3)
   }
 #undef UINET_LEAN_G
 #undef UINET_LEAN
@@ -1023,7 +1026,7 @@ int launch_strided_dense(const void* base, uint64_t stride, uint32_t len, const 
                                              uint32_t, int, hipStream_t);                   \
   template int launch_spans_lean<OffT, LenT>(const void*, const OffT*, const LenT*,         \
                                              const uint32_t*, const uint8_t*, uint16_t*,    \
-                                             uint32_t, uint32_t, int, bool, uint64_t,       \
+                                             uint32_t, uint32_t, int, int, bool, uint64_t,  \
                                              uint32_t, int, hipStream_t);
 UINET_SPANS_INST(uint64_t, uint32_t)
 UINET_SPANS_INST(uint32_t, uint16_t)

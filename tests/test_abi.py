@@ -172,7 +172,7 @@ def test_set_tuning_validation():
     L = u.lib()
     ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_pass", 4), ("chains_long", 0),
           ("chains_long", 16), ("chains_tile", 8), ("xcd_remap", 0), ("host_threads", 64),
-          ("walk_prefetch", 0), ("spans_geo", 0), ("spans_geo", 32 * 16 + 3),
+          ("walk_prefetch", 0), ("spans_geo", 0), ("spans_geo", 32 * 16 + 3), ("spans_geo", 64 * 16 + 9),
           ("host_pin", 1), ("multi_gather", 1), ("spans_pipe", 0), ("spans_pipe", 1)]
     # chains_variant, spans_lut, spans_contig and spans_pipe 2 (k_spans_pp)
     # were removed in round 3; spans_sdesc, host_group and walk_prefetch 2 in

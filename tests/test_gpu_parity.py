@@ -15,7 +15,7 @@ from test_oracle import pcap_cases
 
 pytestmark = pytest.mark.gpu
 
-HINTS = (0, 64, 80, 200, 500, 1500, 9000)  # every kernel geometry
+HINTS = (0, 64, 80, 200, 500, 1500, 4000, 9000)  # every kernel geometry (4000: 64 x 3, 9000: 64 x 9)
 
 
 @pytest.fixture(scope="module")
