@@ -76,9 +76,10 @@ __device__ const SplitWords g_split_words = make_split_words();
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 // A compiler-only memory barrier placed right after a batch of loads: the
 // loads stay where they are issued.  Without it the compiler sinks a step's
-// loads past the previous step's sum whenever that sum has a loop of its own
-// (G = 64: spans longer than one round), which drains the pipeline there.
-// No instruction is emitted and no wait: the barrier names no registers.
+// loads past the previous step's sum whenever that sum branches (k_spans_quad's
+// ballots) or loops (k_spans_lean at 64 lanes: spans longer than one round),
+// which drains the pipeline there.  No instruction is emitted and no wait:
+// the barrier names no registers.
 __device__ __forceinline__ void issued() { asm volatile("" ::: "memory"); }
 // A wave-uniform value the compiler may not reason about (keeps 32-bit
 // compares of a 64-bit value's halves from being merged back into a 64-bit
@@ -591,16 +592,16 @@ __global__ __launch_bounds__(kBlock) void k_spans_quad(
     z.sd = kSeed ? fold16_32(sd) : 0u;
     return z;
   };
-  // The empty asm with a memory clobber keeps the loads where they are: with
-  // no store before their use, the compiler otherwise sinks them below the
-  // previous step's sum (its ballot branches), and the pipeline is gone.
+  // issued() keeps the loads where they are: with no store before their use,
+  // the compiler otherwise sinks them below the previous step's sum (its
+  // ballot branches), and the pipeline is gone.
   auto load = [&](const Z& z, u32x4 (&v)[U]) {
     v[0] = load_chunk(z.c0 + min(16u * gl, z.lb));
     // slot 1 only when some span of the step reaches past 64 B (wave-uniform):
     // aligned 64-B packets never need it
     if constexpr (U == 2)
       if (__ballot(z.e > 64u)) v[1] = load_chunk(z.c0 + min(16u * (4u + gl), z.lb));
-    asm volatile("" ::: "memory");
+    issued();
   };
   // Round 0 of a step from registers.  A step with a span longer than one
   // round (ragged batches) is marked pending and redone whole at the end of

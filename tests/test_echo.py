@@ -59,6 +59,19 @@ def test_echo_oracle_vs_reference(echo, ora, ref):
 @pytest.mark.gpu
 @pytest.mark.parametrize("zero_copy", [False, True])
 def test_echo_gpu(echo, ora, zero_copy):
+    _echo_gpu(echo, ora, zero_copy)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_echo_gpu_config1_full(ora, zero_copy):
+    """Config 1 at its BASELINE size: 65,536 segments (the flow
+    tests/perf/echo_replay.py times), every TX sum equal to the oracle's and
+    every RX verification zero."""
+    _echo_gpu(EchoBatch(65536, seed=11), ora, zero_copy)
+
+
+def _echo_gpu(echo, ora, zero_copy):
     import torch  # noqa: F401  (one HIP runtime)
 
     import libuinet_amd as u
