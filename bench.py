@@ -196,13 +196,13 @@ def dispatched_kernel(cfg: str, api: str, w) -> str:
             and (w["base"] | w["stride"]) % 16):
         return "k_strided_dense"  # launch_strided: small packets off 16-B alignment
     g = 4 if mean <= 64 else 8 if mean <= 224 else 16 if mean <= 720 else 32 if mean <= 1520 else 64
-    u = 2 if g == 4 else 3
+    u = 2 if g == 4 else 9 if mean > 6144 else 3
     if api == "strided" and mean <= 64 and (w["base"] | w["stride"]) % 16 == 0:
         u = 1
     if geo:
         g, u = geo // 16, geo % 16
     if g >= 32:
-        if pipe == 1 and u == 3:
+        if pipe == 1 and u in (3, 9):
             return "k_spans_lean"
         return "k_spans"
     if g == 4 and pipe == 1 and (api == "spans" or u == 1):
@@ -439,6 +439,8 @@ def main():
                  f"torchrun --nproc-per-node {args.gpus} (or drop the launcher)")
     if args.config is None:
         args.config = "4" if distributed else "2"
+    if args.api == "strided" and args.config not in ("2", "2rx", "2s", "2su"):
+        sys.exit(f"bench: --api strided runs configs 2, 2rx, 2s and 2su, not {args.config}")
     # N > 1: every phase has a deadline (libuinet_amd.dist.Watchdog).  A rank
     # stuck in the rendezvous, RCCL init, a step or the parity gather -- or
     # failing in one -- prints one JSON line naming the phase and exits
