@@ -266,6 +266,39 @@ def test_spans_long(torch_dev, ora):
         np.testing.assert_array_equal(host16(got), want)
 
 
+@pytest.mark.parametrize("hint", [1500, 4000, 9000])
+def test_spans_round_edges(torch_dev, ora, hint):
+    """Span lengths at and around the 64-lane geometries' round sizes (3 KB
+    for 64 x 3, 9 KB for 64 x 9: one, two and three rounds and a byte either
+    side) at every head offset 0-15, with seeds, parity and UDP, in batches
+    where the wave's two packets differ (32 lanes) or a wave holds one packet
+    of each length in turn (64 lanes)."""
+    torch = torch_dev
+    rng = np.random.default_rng(4242)
+    edges = [1, 15, 16, 17, 1535, 1536, 1537, 3071, 3072, 3073, 6143, 6144, 6145,
+             9199, 9200, 9201, 9215, 9216, 9217, 18431, 18432, 18433, 27648, 27649]
+    ln = np.array([e for e in edges for _ in range(16)], np.int64)
+    n = ln.size
+    ln = np.concatenate([ln, ln[rng.permutation(n)]])
+    head = np.tile(np.arange(16, dtype=np.int64), 2 * len(edges))
+    arena = rand_arena(4 << 20, 77)
+    off = (rng.integers(0, (arena.size - 28000) // 16, ln.size) * 16 + head).astype(np.int64)
+    seed = rng.integers(0, 2**32, ln.size, dtype=np.uint64).astype(np.uint32)
+    par = rng.integers(0, 2, ln.size).astype(np.uint8)
+    d_arena, d_off, d_ln = dev(torch, arena), dev(torch, off), dev(torch, ln.astype(np.int32))
+    got = u.cksum_spans(d_arena, d_off, d_ln, seed=dev(torch, seed.view(np.int32)),
+                        parity=dev(torch, par), flags=u.F_UDP, len_hint=hint)
+    np.testing.assert_array_equal(host16(got), ora.spans(arena, off, ln, seed, par, u.F_UDP))
+    got = u.cksum_spans(d_arena, d_off, d_ln, len_hint=hint)
+    np.testing.assert_array_equal(host16(got), ora.spans(arena, off, ln))
+    # strided: every packet the same length, at each edge
+    for e in (3072, 3073, 9216, 9217):
+        m = 257
+        got = u.cksum_strided(d_arena[3:], e + 5, e, m)
+        want = ora.spans(arena, 3 + (e + 5) * np.arange(m, dtype=np.int64), np.full(m, e, np.int64))
+        np.testing.assert_array_equal(host16(got), want)
+
+
 def test_spans_zero_and_ff(torch_dev, ora):
     torch = torch_dev
     for fill in (0x00, 0xFF):
