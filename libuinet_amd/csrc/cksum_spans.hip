@@ -28,7 +28,8 @@
 //    of the wave covers whole (slot 1 of a 1500-B packet) skips the table and
 //    the ANDs.  The table is copied from a constant image in global memory.
 //  * Sums.  Each chunk is 4 v_dot2_u32_u16 against (1, 1) into a 32-bit
-//    lane partial (< 2^21, no fold before the reduction).
+//    lane partial (< 2^21 at 3 loads per lane, < 2^23 at 9; no fold before
+//    the reduction).
 //  * Reduction, two steps at once.  A group's partials of packet A (step k)
 //    and packet B (step k + 1) meet in one v_permlane16_swap (G = 32) or
 //    v_permlane32_swap + v_permlane16_swap (G = 64), then 4 DPP row_ror adds:
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
 #pragma unroll
         for (int u = 0; u < kU; ++u)
           r = dot_acc_masked(x[u], lut_m[clampi((int)(e0 - rb - 16u * u * G), 0, 16)], r);
-        acc = fold16_32(acc) + r;  // < 2^21: 64 lanes of it still fit 32 bits
+        acc = fold16_32(acc) + r;  // < 2^23: 64 lanes of it still fit 32 bits
       };
       if constexpr (kP == 1 && kU <= 3) {
         // one packet per wave, 3-KB rounds (spans of 1.5-6 KB mean length, or
@@ -427,7 +428,7 @@ __global__ __launch_bounds__(kBlock) void k_spans_lean(
     t = add_ror<8>(t);
     t = add_ror<4>(t);
     t = add_ror<2>(t);
-    t = add_ror<1>(t);  // every lane: its row's total (< 2^27)
+    t = add_ror<1>(t);  // every lane: its row's total (< 2^27; < 2^29 at kU = 9)
     // row r rotates by 8 when bit r of rowrot is set: rr = 8 in byte r
     const uint32_t rowrot = sA.rot | (sB.rot << (kP == 2 ? 1 : 2));
     const uint32_t rr = ((rowrot * 0x00204081u) & 0x01010101u) << 3;
