@@ -1,0 +1,125 @@
+"""Randomised differential test of the device-resident entry points against the
+oracle: every trial draws an API (spans wide / packed, strided, chains wide /
+packed), a batch shape (counts, length families from empty to 20 KB, head
+offsets, lengths and skips that cut chains short), a length hint that may not
+match the batch, flags, seeds and parity, and a setting of every performance
+knob (which must never change a result: include/uinet_cksum.h).  Seeded, so a
+failure names its trial and replays."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import libuinet_amd as u
+
+from test_gpu_parity import dev, host16, rand_arena
+
+pytestmark = pytest.mark.gpu
+
+DEFAULTS = {"blocks_per_cu": 0, "chains_pass": 2, "chains_long": 128, "chains_tile": 0,
+            "xcd_remap": 1, "spans_geo": 0, "spans_pipe": 1}
+KNOBS = {"blocks_per_cu": [0, 0, 1, 3, 64], "chains_pass": [2, 2, 4], "chains_long": [128, 0, 16],
+         "chains_tile": [0, 8, 32], "xcd_remap": [1, 0], "spans_pipe": [1, 1, 0],
+         "spans_geo": [0] * 6 + [4 * 16 + 1, 4 * 16 + 2, 8 * 16 + 1, 8 * 16 + 2, 16 * 16 + 3,
+                                 32 * 16 + 3, 64 * 16 + 2, 64 * 16 + 3, 64 * 16 + 9]}
+HINTS = (0, 64, 80, 200, 500, 1500, 4000, 9000)
+ARENA = 8 << 20
+TRIALS = int(os.environ.get("UINET_FUZZ_TRIALS", "300"))  # longer hunts: set it
+
+
+def _lengths(rng, n):
+    fam = rng.integers(0, 5)
+    hi = (64, 300, 2000, 9300, 20000)[fam]
+    ln = rng.integers(0, hi + 1, n)
+    edge = rng.random(n) < 0.05
+    ln[edge] = rng.choice([0, 1, 15, 16, 17, 63, 64, 65, 1500, 3072, 9216, 9217], int(edge.sum()))
+    return ln.astype(np.int64)
+
+
+def _trial(torch, ora, arena, d_arena, t):
+    rng = np.random.default_rng(90000 + t)
+    knobs = {k: int(rng.choice(vals)) for k, vals in KNOBS.items()}
+    for k, v in knobs.items():
+        u.set_tuning(k, v)
+    api = ("spans", "spans32", "strided", "chains", "chains32")[rng.integers(0, 5)]
+    n = int(rng.choice([1, 2, 3, 63, 64, 65, int(rng.integers(1, 3000))]))
+    hint = int(rng.choice(HINTS)) if rng.random() < 0.8 else int(rng.integers(0, 12000))
+    flags = int(rng.choice([0, u.F_UDP, u.F_NO_COMPLEMENT]))
+    seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if rng.random() < 0.5 else None
+    d_seed = dev(torch, seed.view(np.int32)) if seed is not None else None
+    if api in ("spans", "spans32", "strided"):
+        if api == "strided":
+            length = int(_lengths(rng, 1)[0])
+            stride = length + int(rng.integers(0, 40))
+            n = max(1, min(n, (ARENA - 64) // max(stride, 1)))
+            seed = seed[:n] if seed is not None else None
+            d_seed = dev(torch, seed.view(np.int32)) if seed is not None else None
+            base = int(rng.integers(0, 64))
+            got = u.cksum_strided(d_arena[base:], stride, length, n, seed=d_seed, flags=flags)
+            off = base + stride * np.arange(n, dtype=np.int64)
+            want = ora.spans(arena, off, np.full(n, length, np.int64), seed, None, flags)
+        else:
+            ln = _lengths(rng, n)
+            off = rng.integers(0, ARENA - 20001, n).astype(np.int64)
+            par = rng.integers(0, 2, n).astype(np.uint8) if rng.random() < 0.5 else None
+            d_par = dev(torch, par) if par is not None else None
+            if api == "spans32":
+                po, pl = u.pack_segments(off, ln.astype(np.int32))
+                d_off, d_ln = dev(torch, po), dev(torch, pl)
+            else:
+                d_off, d_ln = dev(torch, off), dev(torch, ln.astype(np.int32))
+            got = u.cksum_spans(d_arena, d_off, d_ln, seed=d_seed, parity=d_par, flags=flags,
+                                len_hint=hint)
+            want = ora.spans(arena, off, ln, seed, par, flags)
+    else:
+        nseg = rng.integers(0 if rng.random() < 0.1 else 1, int(rng.choice([2, 8, 40])) + 1, n)
+        nseg[0] = max(nseg[0], 1)  # at least one segment in the batch
+        pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+        s = int(pkt_seg[-1])
+        seg_len = _lengths(rng, s)
+        if rng.random() < 0.5:  # segments laid out in order, 0-7 B apart (config-3 shape)
+            gaps = rng.integers(0, 8, s)
+            seg_off = np.cumsum(np.concatenate([[int(rng.integers(0, 16))], (seg_len + gaps)[:-1]]))
+            seg_off = (seg_off % (ARENA - 20001)).astype(np.int64)
+        else:
+            seg_off = rng.integers(0, ARENA - 20001, s).astype(np.int64)
+        cs = np.concatenate([[0], np.cumsum(seg_len)])
+        tot = cs[pkt_seg[1:]] - cs[pkt_seg[:-1]]
+        length = skip = None
+        if rng.random() < 0.5:
+            length = np.maximum(0, tot + rng.integers(-40, 41, n)).astype(np.int64)
+        if rng.random() < 0.5:
+            skip = np.minimum(rng.integers(0, 61, n), tot if length is None else length)
+            skip = skip.astype(np.int64)
+        if api == "chains32":
+            so, sl = u.pack_segments(seg_off, seg_len.astype(np.int32))
+            d_so, d_sl = dev(torch, so), dev(torch, sl)
+        else:
+            d_so, d_sl = dev(torch, seg_off), dev(torch, seg_len.astype(np.int32))
+        got = u.cksum_chains(d_arena, d_so, d_sl, dev(torch, pkt_seg.astype(np.int32)),
+                             length=dev(torch, length.astype(np.int32)) if length is not None else None,
+                             skip=dev(torch, skip.astype(np.int32)) if skip is not None else None,
+                             seed=d_seed, flags=flags, len_hint=hint)
+        want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed,
+                          flags=flags)
+    bad = np.flatnonzero(host16(got) != want)
+    _trial.packets = getattr(_trial, "packets", 0) + n
+    assert bad.size == 0, (f"trial {t}: api={api} n={n} hint={hint} flags={flags} "
+                           f"knobs={knobs} first mismatches {bad[:5].tolist()}")
+
+
+def test_fuzz_device_entry_points(ora):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    arena = rand_arena(ARENA, 2024)
+    d_arena = dev(torch, arena)
+    try:
+        for t in range(TRIALS):
+            _trial(torch, ora, arena, d_arena, t)
+        print(f"fuzz: {TRIALS} trials, {_trial.packets} packets")
+    finally:
+        for k, v in DEFAULTS.items():
+            u.set_tuning(k, v)
