@@ -123,3 +123,68 @@ def test_fuzz_device_entry_points(ora):
     finally:
         for k, v in DEFAULTS.items():
             u.set_tuning(k, v)
+
+
+HOST_DEFAULTS = {"host_threads": min(16, os.cpu_count() or 1), "walk_prefetch": 1, "host_pin": 0}
+
+
+def _host_trial(ora, arena, t):
+    from libuinet_amd.mbuf import MbufChains
+
+    rng = np.random.default_rng(70000 + t)
+    u.set_tuning("host_threads", int(rng.choice([1, 2, 5, 16])))
+    u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
+    u.set_tuning("host_pin", int(rng.integers(0, 2)))
+    n = int(rng.choice([1, 7, 64, int(rng.integers(1, 2500))]))
+    nseg = rng.integers(1, int(rng.choice([2, 6, 30])) + 1, n)  # a chain is >= 1 mbuf
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = _lengths(rng, s)
+    if rng.random() < 0.15:  # pieces past 65535 B: the zero-copy path's wide descriptors
+        seg_len[rng.integers(0, s)] = int(rng.integers(65536, 90000))
+    seg_off = rng.integers(0, ARENA - 90001, s).astype(np.int64)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    cs = np.concatenate([[0], np.cumsum(seg_len)])
+    tot = cs[pkt_seg[1:]] - cs[pkt_seg[:-1]]
+    zero_copy = rng.random() < 0.5
+    if zero_copy:
+        u.register_host(arena)
+    try:
+        if rng.random() < 0.7:
+            length = np.maximum(0, tot + rng.integers(-30, 31, n)).astype(np.int64)
+            skip = np.minimum(rng.integers(0, 41, n), length).astype(np.int64)
+            got = u.in_cksum_skip_batch(ch.heads, length, skip)
+            want = ora.skip_batch(ch.heads, length, skip)
+            what = "skip"
+        else:
+            off0 = np.minimum(rng.integers(0, 41, n), tot)
+            plen = np.maximum(0, tot - off0 - rng.integers(0, 20, n))
+            src, dst = (rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) for _ in range(2))
+            proto = rng.choice(np.array([6, 17], np.uint8), n)
+            got = u.in_cksum_pseudo_header_batch(ch.heads, plen, off0, src, dst, proto)
+            want = ora.pseudo_header_batch(ch.heads, plen, off0, src, dst, proto)
+            what = "pseudo"
+    finally:
+        if zero_copy:
+            u.unregister_host(arena)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (f"host trial {t}: {what} n={n} zero_copy={zero_copy} "
+                           f"first mismatches {bad[:5].tolist()}")
+    return n
+
+
+def test_fuzz_host_batches(ora):
+    """The host-mbuf batch API (in_cksum_skip_batch, in_cksum_pseudo_header_batch)
+    over random chains, staged and zero-copy, under random host-pool knobs."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    arena = rand_arena(ARENA, 2025)
+    packets = 0
+    try:
+        for t in range(max(1, TRIALS // 3)):
+            packets += _host_trial(ora, arena, t)
+        print(f"host fuzz: {max(1, TRIALS // 3)} trials, {packets} packets")
+    finally:
+        for k, v in HOST_DEFAULTS.items():
+            u.set_tuning(k, v)
