@@ -188,3 +188,62 @@ def test_fuzz_host_batches(ora):
     finally:
         for k, v in HOST_DEFAULTS.items():
             u.set_tuning(k, v)
+
+
+def test_fuzz_offload_hooks(ora):
+    """The RX / TX driver hooks over random frame batches (IPv4 and IPv6 in random
+    proportions, with and without the link header, random corruption), staged and
+    zero-copy, under random host-pool knobs: status, packet bytes and m_pkthdr
+    marks equal the oracle's."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from libuinet_amd.frames import FrameBatch, pkthdr_fields
+
+    frames = 0
+    try:
+        for t in range(max(1, TRIALS // 10)):
+            rng = np.random.default_rng(50000 + t)
+            u.set_tuning("host_threads", int(rng.choice([1, 3, 16])))
+            u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
+            n = int(rng.choice([1, 2, int(rng.integers(1, 1500))]))
+            l2 = bool(rng.integers(0, 2))
+            l2len = -1 if l2 else 0
+            ipv6 = float(rng.choice([0.0, 0.3, 1.0]))
+            seed = int(rng.integers(0, 2**31))
+            a = FrameBatch(n, seed=seed, l2=l2, ipv6=ipv6)
+            b = FrameBatch(n, seed=seed, l2=l2, ipv6=ipv6)
+            zc = bool(rng.integers(0, 2))
+            if zc:
+                u.register_host(a.arena)
+            try:
+                st_g = u.tx_offload(a.tx.heads, l2len)
+            finally:
+                if zc:
+                    u.unregister_host(a.arena)
+            st_o = ora.tx_offload(b.tx.heads, l2len)
+            ctx = f"offload trial {t}: n={n} l2={l2} ipv6={ipv6} zero_copy={zc}"
+            assert np.array_equal(st_g, st_o), ctx + " (TX status)"
+            assert np.array_equal(a.arena, b.arena), ctx + " (TX bytes)"
+            for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
+                assert np.array_equal(x, y), ctx + " (TX marks)"
+            corrupt = float(rng.choice([0.0, 0.05, 0.5]))
+            rs = int(rng.integers(0, 2**31))
+            rx_a, arena_a, _ = a.rx(seed=rs, corrupt=corrupt)
+            rx_b, _, _ = b.rx(seed=rs, corrupt=corrupt)
+            if zc:
+                u.register_host(arena_a)
+            try:
+                st_g = u.rx_offload(rx_a.heads, l2len)
+            finally:
+                if zc:
+                    u.unregister_host(arena_a)
+            st_o = ora.rx_offload(rx_b.heads, l2len)
+            assert np.array_equal(st_g, st_o), ctx + f" corrupt={corrupt} (RX status)"
+            for x, y in zip(pkthdr_fields(rx_a), pkthdr_fields(rx_b)):
+                assert np.array_equal(x, y), ctx + f" corrupt={corrupt} (RX marks)"
+            frames += n
+        print(f"offload fuzz: {max(1, TRIALS // 10)} trials, {frames} frames each way")
+    finally:
+        for k, v in HOST_DEFAULTS.items():
+            u.set_tuning(k, v)
