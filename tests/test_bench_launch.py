@@ -32,6 +32,17 @@ def test_world_size_mismatch_is_an_error():
     assert "WORLD_SIZE=3" in r.stderr
 
 
+def test_strided_api_only_for_strided_configs():
+    """--api strided measures packets at a fixed stride (configs 2, 2rx, 2s,
+    2su); asked of another config the bench stops instead of timing the span
+    API under a strided label."""
+    for cfg in ("3", "4", "5", "5tso"):
+        r = _run(["--config", cfg, "--api", "strided", "--dry-run"])
+        assert r.returncode != 0 and "--api strided" in r.stderr, (cfg, r.stderr[-500:])
+    r = _run(["--config", "2su", "--api", "strided", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
 def test_gpus_n_spawns_n_ranks_with_config4_default():
     r = _run(["--gpus", "3", "--dry-run"])
     assert r.returncode == 0, r.stderr[-2000:]
