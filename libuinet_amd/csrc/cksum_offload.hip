@@ -18,7 +18,11 @@
 // The host parses headers (a few bytes per packet, already in cache from the
 // driver) and writes flags; every byte sum is a GPU job (host_batch.h).
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <chrono>
 
 #include <vector>
 
@@ -250,6 +254,33 @@ Job rx6_job(const MbufHdr* m, const Ip6& ip, uint8_t* st) {
   return Job{m, ip.l3 + 40 + ip.plen, ip.l3 + off, pseudo6_seed(ip, (uint32_t)tlen, nxt)};
 }
 
+// UINET_CKSUM_TRACE_HOST=1: the hooks' phase times on stderr (tools only;
+// run_jobs prints its own walk / pack / launch split under the same switch).
+struct PhaseTrace {
+  using clk = std::chrono::steady_clock;
+  const char* what;
+  bool on;
+  clk::time_point t0, t1, t2;
+  explicit PhaseTrace(const char* w) : what(w), on(getenv("UINET_CKSUM_TRACE_HOST") != nullptr) {
+    if (on) t0 = clk::now();
+  }
+  void parsed() {
+    if (on) t1 = clk::now();
+  }
+  void summed() {
+    if (on) t2 = clk::now();
+  }
+  void done(int n) {
+    if (!on) return;
+    const clk::time_point t3 = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    fprintf(stderr, "uinet_cksum offload %s: n=%d | parse %.3f ms, jobs %.3f ms, apply %.3f ms\n", what,
+            n, ms(t0, t1), ms(t1, t2), ms(t2, t3));
+  }
+};
+
 thread_local std::vector<Job> t_jobs;
 thread_local std::vector<uint16_t> t_res;
 thread_local std::vector<RxPlan> t_rx;
@@ -276,6 +307,7 @@ extern "C" {
 int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
   if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
+  PhaseTrace tr("rx");
   std::vector<Job>& jobs = t_jobs;
   std::vector<RxPlan>& plan = t_rx;
   jobs.assign(2 * (size_t)n, Job{nullptr, 0, 0, 0u});
@@ -326,10 +358,12 @@ int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
                                  pseudo_seed(ip.src, ip.dst, ip.proto, plen)};
     }
   });
+  tr.parsed();
   std::vector<uint16_t>& res = t_res;
   res.resize(jobs.size());
   const int rc = run_jobs(jobs.data(), (int)jobs.size(), res.data());
   if (rc) return rc;
+  tr.summed();
   for_chunks(n, [&](int i0, int i1) {
     for (int i = i0; i < i1; i++) {
       RxPlan& p = plan[(size_t)i];
@@ -352,12 +386,14 @@ int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
       if (status) status[i] = p.st;
     }
   });
+  tr.done(n);
   return UINET_CKSUM_OK;
 }
 
 int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
   if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
+  PhaseTrace tr("tx");
   std::vector<Job>& jobs = t_jobs;
   std::vector<TxPlan>& plan = t_tx;
   jobs.assign(2 * (size_t)n, Job{nullptr, 0, 0, 0u});
@@ -418,10 +454,12 @@ int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
       }
     }
   });
+  tr.parsed();
   std::vector<uint16_t>& res = t_res;
   res.resize(jobs.size());
   const int rc = run_jobs(jobs.data(), (int)jobs.size(), res.data());
   if (rc) return rc;
+  tr.summed();
   for_chunks(n, [&](int i0, int i1) {
     for (int i = i0; i < i1; i++) {
       TxPlan& p = plan[(size_t)i];
@@ -446,6 +484,7 @@ int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
       if (status) status[i] = p.st;
     }
   });
+  tr.done(n);
   return UINET_CKSUM_OK;
 }
 
