@@ -613,6 +613,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   // of `threads`, so packing group g+1 overlaps the copy of group g
   int cs = (n + threads * 16 - 1) / (threads * 16);
   if (cs < kChunkMin) cs = kChunkMin;
+  cs = (cs + 1) & ~1;  // even: no chunk splits a job pair 2k, 2k + 1 (run_jobs_made)
   const int nch = (n + cs - 1) / cs;
   Batch& B = t_batch;
   if ((int)B.chunks.size() < nch) B.chunks.resize((size_t)nch);
@@ -808,6 +809,15 @@ int run_jobs(const Job* jobs, int n, uint16_t* out) {
     w.walk_skip(jobs[i].m, jobs[i].len, jobs[i].skip);
     return jobs[i].seed;
   }, [&](int i) { return ChainRef{jobs[i].m, (long)jobs[i].len}; });
+}
+
+int run_jobs_made(int n, JobMaker make, JobFirst first, void* ctx, uint16_t* out) {
+  if (n > 0 && (!make || !first || !out)) return UINET_CKSUM_EINVAL;
+  return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
+    const Job j = make(ctx, i);
+    w.walk_skip(j.m, j.len, j.skip);
+    return j.seed;
+  }, [&](int i) { return ChainRef{first(ctx, i), 0x7fffffffL}; });  // chased like a whole chain
 }
 
 namespace {

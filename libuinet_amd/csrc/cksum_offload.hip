@@ -281,7 +281,7 @@ struct PhaseTrace {
   }
 };
 
-thread_local std::vector<Job> t_jobs;
+thread_local std::vector<Job> t_l4;
 thread_local std::vector<uint16_t> t_res;
 thread_local std::vector<RxPlan> t_rx;
 thread_local std::vector<TxPlan> t_tx;
@@ -297,6 +297,141 @@ void for_chunks(int n, F&& f) {
                   tuning().host_pin != 0);
 }
 
+// Packet k of a hook's batch owns jobs 2k (IP header) and 2k + 1 (TCP / UDP);
+// the hook's parse runs when the batch walk reaches job 2k (run_jobs_made), so
+// each packet's headers are read once, on the thread that then walks its
+// chains.  Parsing is idempotent (a staged re-walk parses again).
+struct HookCtx {
+  struct mbuf* const* mv;
+  int l2len;
+  void* plan;  // RxPlan* or TxPlan*
+  Job* l4;     // job 2k + 1 of packet k, made with job 2k
+};
+const MbufHdr* hook_first(void* ctx, int i) {
+  return reinterpret_cast<const MbufHdr*>(static_cast<HookCtx*>(ctx)->mv[i >> 1]);
+}
+
+// RX: ip_input.c:460-471, tcp_input.c:697-718, udp_usrreq.c:404-449 and the
+// IPv6 forms (rx6_job).  Returns the IP-header job; the L4 job goes to *l4.
+Job rx_parse(const MbufHdr* m, int l2len, RxPlan& p, Job* l4) {
+  const Job none{nullptr, 0, 0, 0u};
+  p = RxPlan();
+  *l4 = none;
+  int l3 = 0;
+  const int ver = m ? l3_locate(m, l2len, &l3) : 0;
+  if (ver == 6) {
+    Ip6 ip6;
+    if (!parse_ip6(m, l3, &ip6)) return none;
+    p.st |= UINET_RX_IPV6;
+    const Job j = rx6_job(m, ip6, &p.st);
+    if (j.m) {
+      p.l4_job = true;
+      *l4 = j;
+    }
+    return none;
+  }
+  if (ver != 4 || !parse_ip4(m, l3, &p.ip)) return none;
+  const Ip4& ip = p.ip;
+  p.st |= UINET_RX_IPV4;
+  p.ip_job = true;  // in_cksum(m, hlen) over the header (ip_input.c:463-467)
+  const Job hdr{m, ip.l3 + ip.hl, ip.l3, 0u};
+  if (ip.frag) {
+    p.st |= UINET_RX_FRAG;
+    return hdr;
+  }
+  if (ip.ip_len < ip.hl || chain_len(m) < (long)ip.l3 + ip.ip_len) return hdr;
+  int plen = ip.ip_len - ip.hl;
+  if (ip.proto == 6) {  // tcp_input.c:711-713: tlen = ip_len - off0
+  } else if (ip.proto == 17) {
+    if (ip.l4_have < 8) return hdr;
+    if (be16(ip.l4 + 6) == 0) {  // uh_sum 0: no checksum (udp_usrreq.c:427,450)
+      p.st |= UINET_RX_NOSUM;
+      return hdr;
+    }
+    const int ulen = be16(ip.l4 + 4);  // udp_usrreq.c:404-412
+    if (ulen > plen || ulen < 8) return hdr;
+    plen = ulen;
+  } else {
+    return hdr;
+  }
+  p.l4_job = true;
+  *l4 = Job{m, ip.l3 + ip.hl + plen, ip.l3 + ip.hl, pseudo_seed(ip.src, ip.dst, ip.proto, plen)};
+  return hdr;
+}
+Job rx_make(void* ctx, int i) {
+  HookCtx& c = *static_cast<HookCtx*>(ctx);
+  const int k = i >> 1;
+  if (i & 1) return c.l4[k];
+  return rx_parse(reinterpret_cast<const MbufHdr*>(c.mv[k]), c.l2len,
+                  static_cast<RxPlan*>(c.plan)[k], &c.l4[k]);
+}
+
+// TX: ip_output.c:645-667,953-976 and ip6_output.c:188-209,966-988.  Zeroes
+// ip_sum before the header job reads it (ip_output.c:665-667).
+Job tx_parse(MbufHdr* m, int l2len, TxPlan& p, Job* l4) {
+  const Job none{nullptr, 0, 0, 0u};
+  p = TxPlan();
+  *l4 = none;
+  if (!m || !(m->m_flags & kMPktHdr)) {
+    p.st = UINET_TX_SKIP;
+    return none;
+  }
+  const int fl = pkthdr_of(m)->csum_flags;
+  int l3 = 0;
+  const int ver = (fl & kCsumTso) ? 0 : l3_locate(m, l2len, &l3);
+  if (ver == 6) {  // in6_delayed_cksum, ip6_output.c:188-209,978-981
+    // As an offloading NIC must (ip6_output.c:966-981 leaves CSUM_*_IPV6 to a
+    // driver that advertises it, extension headers or not), the transport is
+    // found past the extension headers; the seed already in its checksum
+    // field holds the final destination.
+    Ip6 ip6;
+    int off = 40, nxt = 0;
+    if (!(fl & (kCsumTcpIpv6 | kCsumUdpIpv6)) || !parse_ip6(m, l3, &ip6) || ip6.plen == 0 ||
+        ip6_walk(m, ip6, false, &off, &nxt) != 1) {
+      p.st = UINET_TX_SKIP;
+      return none;
+    }
+    p.st = UINET_TX_IPV6;
+    p.udp = (fl & kCsumUdpIpv6) != 0;
+    p.clear = kCsumTcpIpv6 | kCsumUdpIpv6;
+    p.l4_store = l3 + off + pkthdr_of(m)->csum_data;
+    p.l4_job = true;
+    *l4 = Job{m, l3 + 40 + ip6.plen, l3 + off, 0u};
+    return none;
+  }
+  Ip4 ip;
+  if (ver != 4 || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) || !parse_ip4(m, l3, &ip)) {
+    p.st = UINET_TX_SKIP;
+    return none;
+  }
+  if ((fl & kCsumIp) && ip.l3 + 12 > m->m_len) {
+    p.st = UINET_TX_SKIP;  // header not in the first mbuf: leave it to the stack
+    return none;
+  }
+  if (fl & (kCsumTcp | kCsumUdp)) {  // in_delayed_cksum, ip_output.c:958-963
+    p.udp = (fl & kCsumUdp) != 0;
+    p.clear = kCsumTcp | kCsumUdp;
+    p.l4_store = ip.l3 + ip.hl + pkthdr_of(m)->csum_data;
+    p.l4_job = true;
+    *l4 = Job{m, ip.l3 + ip.ip_len, ip.l3 + ip.hl, 0u};
+  }
+  if (fl & kCsumIp) {  // ip_output.c:665-667: ip_sum = 0, then in_cksum(m, hlen)
+    m->m_data[ip.l3 + 10] = 0;
+    m->m_data[ip.l3 + 11] = 0;
+    p.ip_l3 = ip.l3;
+    p.ip_job = true;
+    return Job{m, ip.l3 + ip.hl, ip.l3, 0u};
+  }
+  return none;
+}
+Job tx_make(void* ctx, int i) {
+  HookCtx& c = *static_cast<HookCtx*>(ctx);
+  const int k = i >> 1;
+  if (i & 1) return c.l4[k];
+  return tx_parse(reinterpret_cast<MbufHdr*>(c.mv[k]), c.l2len, static_cast<TxPlan*>(c.plan)[k],
+                  &c.l4[k]);
+}
+
 }  // namespace
 }  // namespace uinet
 
@@ -308,60 +443,15 @@ int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
   if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
   PhaseTrace tr("rx");
-  std::vector<Job>& jobs = t_jobs;
   std::vector<RxPlan>& plan = t_rx;
-  jobs.assign(2 * (size_t)n, Job{nullptr, 0, 0, 0u});
-  plan.assign((size_t)n, RxPlan());
-  for_chunks(n, [&](int i0, int i1) {
-    for (int i = i0; i < i1; i++) {
-      const MbufHdr* m = reinterpret_cast<const MbufHdr*>(mv[i]);
-      RxPlan& p = plan[(size_t)i];
-      int l3 = 0;
-      const int ver = m ? l3_locate(m, l2len, &l3) : 0;
-      if (ver == 6) {
-        Ip6 ip6;
-        if (!parse_ip6(m, l3, &ip6)) continue;
-        p.st |= UINET_RX_IPV6;
-        const Job j = rx6_job(m, ip6, &p.st);
-        if (j.m) {
-          p.l4_job = true;
-          jobs[2 * (size_t)i + 1] = j;
-        }
-        continue;
-      }
-      if (ver != 4 || !parse_ip4(m, l3, &p.ip)) continue;
-      const Ip4& ip = p.ip;
-      p.st |= UINET_RX_IPV4;
-      p.ip_job = true;  // in_cksum(m, hlen) over the header (ip_input.c:463-467)
-      jobs[2 * (size_t)i] = {m, ip.l3 + ip.hl, ip.l3, 0u};
-      if (ip.frag) {
-        p.st |= UINET_RX_FRAG;
-        continue;
-      }
-      if (ip.ip_len < ip.hl || chain_len(m) < (long)ip.l3 + ip.ip_len) continue;
-      int plen = ip.ip_len - ip.hl;
-      if (ip.proto == 6) {  // tcp_input.c:711-713: tlen = ip_len - off0
-      } else if (ip.proto == 17) {
-        if (ip.l4_have < 8) continue;
-        if (be16(ip.l4 + 6) == 0) {  // uh_sum 0: no checksum (udp_usrreq.c:427,450)
-          p.st |= UINET_RX_NOSUM;
-          continue;
-        }
-        const int ulen = be16(ip.l4 + 4);  // udp_usrreq.c:404-412
-        if (ulen > plen || ulen < 8) continue;
-        plen = ulen;
-      } else {
-        continue;
-      }
-      p.l4_job = true;
-      jobs[2 * (size_t)i + 1] = {m, ip.l3 + ip.hl + plen, ip.l3 + ip.hl,
-                                 pseudo_seed(ip.src, ip.dst, ip.proto, plen)};
-    }
-  });
-  tr.parsed();
+  std::vector<Job>& l4 = t_l4;
+  plan.resize((size_t)n);
+  l4.resize((size_t)n);
+  HookCtx ctx{mv, l2len, plan.data(), l4.data()};
+  tr.parsed();  // parsing runs inside the walk
   std::vector<uint16_t>& res = t_res;
-  res.resize(jobs.size());
-  const int rc = run_jobs(jobs.data(), (int)jobs.size(), res.data());
+  res.resize(2 * (size_t)n);
+  const int rc = run_jobs_made(2 * n, rx_make, hook_first, &ctx, res.data());
   if (rc) return rc;
   tr.summed();
   for_chunks(n, [&](int i0, int i1) {
@@ -394,70 +484,15 @@ int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
   if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
   PhaseTrace tr("tx");
-  std::vector<Job>& jobs = t_jobs;
   std::vector<TxPlan>& plan = t_tx;
-  jobs.assign(2 * (size_t)n, Job{nullptr, 0, 0, 0u});
-  plan.assign((size_t)n, TxPlan());
-  for_chunks(n, [&](int i0, int i1) {
-    for (int i = i0; i < i1; i++) {
-      MbufHdr* m = reinterpret_cast<MbufHdr*>(mv[i]);
-      TxPlan& p = plan[(size_t)i];
-      if (!m || !(m->m_flags & kMPktHdr)) {
-        p.st = UINET_TX_SKIP;
-        continue;
-      }
-      const int fl = pkthdr_of(m)->csum_flags;
-      int l3 = 0;
-      const int ver = (fl & kCsumTso) ? 0 : l3_locate(m, l2len, &l3);
-      if (ver == 6) {  // in6_delayed_cksum, ip6_output.c:188-209,978-981
-        // As an offloading NIC must (ip6_output.c:966-981 leaves CSUM_*_IPV6
-        // to a driver that advertises it, extension headers or not), the
-        // transport is found past the extension headers; the seed already
-        // in its checksum field holds the final destination.
-        Ip6 ip6;
-        int off = 40, nxt = 0;
-        if (!(fl & (kCsumTcpIpv6 | kCsumUdpIpv6)) || !parse_ip6(m, l3, &ip6) || ip6.plen == 0 ||
-            ip6_walk(m, ip6, false, &off, &nxt) != 1) {
-          p.st = UINET_TX_SKIP;
-          continue;
-        }
-        p.st = UINET_TX_IPV6;
-        p.udp = (fl & kCsumUdpIpv6) != 0;
-        p.clear = kCsumTcpIpv6 | kCsumUdpIpv6;
-        p.l4_store = l3 + off + pkthdr_of(m)->csum_data;
-        p.l4_job = true;
-        jobs[2 * (size_t)i + 1] = {m, l3 + 40 + ip6.plen, l3 + off, 0u};
-        continue;
-      }
-      Ip4 ip;
-      if (ver != 4 || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) || !parse_ip4(m, l3, &ip)) {
-        p.st = UINET_TX_SKIP;
-        continue;
-      }
-      if ((fl & kCsumIp) && ip.l3 + 12 > m->m_len) {
-        p.st = UINET_TX_SKIP;  // header not in the first mbuf: leave it to the stack
-        continue;
-      }
-      if (fl & (kCsumTcp | kCsumUdp)) {  // in_delayed_cksum, ip_output.c:958-963
-        p.udp = (fl & kCsumUdp) != 0;
-        p.clear = kCsumTcp | kCsumUdp;
-        p.l4_store = ip.l3 + ip.hl + pkthdr_of(m)->csum_data;
-        p.l4_job = true;
-        jobs[2 * (size_t)i + 1] = {m, ip.l3 + ip.ip_len, ip.l3 + ip.hl, 0u};
-      }
-      if (fl & kCsumIp) {  // ip_output.c:665-667: ip_sum = 0, then in_cksum(m, hlen)
-        m->m_data[ip.l3 + 10] = 0;
-        m->m_data[ip.l3 + 11] = 0;
-        p.ip_l3 = ip.l3;
-        p.ip_job = true;
-        jobs[2 * (size_t)i] = {m, ip.l3 + ip.hl, ip.l3, 0u};
-      }
-    }
-  });
-  tr.parsed();
+  std::vector<Job>& l4 = t_l4;
+  plan.resize((size_t)n);
+  l4.resize((size_t)n);
+  HookCtx ctx{mv, l2len, plan.data(), l4.data()};
+  tr.parsed();  // parsing runs inside the walk
   std::vector<uint16_t>& res = t_res;
-  res.resize(jobs.size());
-  const int rc = run_jobs(jobs.data(), (int)jobs.size(), res.data());
+  res.resize(2 * (size_t)n);
+  const int rc = run_jobs_made(2 * n, tx_make, hook_first, &ctx, res.data());
   if (rc) return rc;
   tr.summed();
   for_chunks(n, [&](int i0, int i1) {

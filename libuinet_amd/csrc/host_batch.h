@@ -57,6 +57,18 @@ struct Job {
 // launch).  Returns a UINET_CKSUM_* code.
 int run_jobs(const Job* jobs, int n, uint16_t* out);
 
+// The same for jobs made while the batch is walked: make(ctx, i) returns job
+// i on the walking thread, just before its chain is walked, so a caller that
+// derives jobs from packet headers reads each header once, while its lines
+// are being fetched anyway.  Jobs 2k and 2k + 1 are made on one thread, in
+// that order (a walk chunk never splits such a pair), and a job may be made
+// more than once (a zero-copy batch that has to be staged is walked again):
+// make must be idempotent.  first(ctx, i) is job i's first mbuf (prefetched
+// a few jobs ahead), without making the job.
+typedef Job (*JobMaker)(void* ctx, int i);
+typedef const MbufHdr* (*JobFirst)(void* ctx, int i);
+int run_jobs_made(int n, JobMaker make, JobFirst first, void* ctx, uint16_t* out);
+
 // The per-call ABI's host fold (cksum_percall.cpp): one chain on the calling
 // thread, no device involved, no error path (like the reference).
 uint16_t host_cksum_skip(const MbufHdr* m, long len, long skip, uint32_t seed);
