@@ -303,10 +303,23 @@ void for_chunks(int n, F&& f) {
 // chains.  Parsing is idempotent (a staged re-walk parses again).
 struct HookCtx {
   struct mbuf* const* mv;
+  int n;
   int l2len;
   void* plan;  // RxPlan* or TxPlan*
   Job* l4;     // job 2k + 1 of packet k, made with job 2k
 };
+// The RX parse reads each packet's first data line(s) (link, IP and transport
+// headers, in a cluster apart from the mbuf): request packet k + 4's while
+// packet k is parsed.  Its mbuf header was requested 4 packets earlier (the
+// walk's prefetch runs 8 packets ahead).  RX 17 % faster (r04hk3).
+constexpr int kDataAhead = 4;
+inline void prefetch_headers(const HookCtx& c, int k) {
+  const int a = k + kDataAhead;
+  if (a >= c.n || !c.mv[a]) return;
+  const uint8_t* d = reinterpret_cast<const MbufHdr*>(c.mv[a])->m_data;
+  __builtin_prefetch(d, 0, 3);
+  __builtin_prefetch(d + 64, 0, 3);
+}
 const MbufHdr* hook_first(void* ctx, int i) {
   return reinterpret_cast<const MbufHdr*>(static_cast<HookCtx*>(ctx)->mv[i >> 1]);
 }
@@ -362,6 +375,7 @@ Job rx_make(void* ctx, int i) {
   HookCtx& c = *static_cast<HookCtx*>(ctx);
   const int k = i >> 1;
   if (i & 1) return c.l4[k];
+  prefetch_headers(c, k);
   return rx_parse(reinterpret_cast<const MbufHdr*>(c.mv[k]), c.l2len,
                   static_cast<RxPlan*>(c.plan)[k], &c.l4[k]);
 }
@@ -428,6 +442,8 @@ Job tx_make(void* ctx, int i) {
   HookCtx& c = *static_cast<HookCtx*>(ctx);
   const int k = i >> 1;
   if (i & 1) return c.l4[k];
+  // no data prefetch: a TX packet's headers sit in its first mbuf (m_pktdat),
+  // which the walk's own prefetch brings in (measured 9 % slower with it, r04hk3)
   return tx_parse(reinterpret_cast<MbufHdr*>(c.mv[k]), c.l2len, static_cast<TxPlan*>(c.plan)[k],
                   &c.l4[k]);
 }
@@ -447,7 +463,7 @@ int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
   std::vector<Job>& l4 = t_l4;
   plan.resize((size_t)n);
   l4.resize((size_t)n);
-  HookCtx ctx{mv, l2len, plan.data(), l4.data()};
+  HookCtx ctx{mv, n, l2len, plan.data(), l4.data()};
   tr.parsed();  // parsing runs inside the walk
   std::vector<uint16_t>& res = t_res;
   res.resize(2 * (size_t)n);
@@ -488,7 +504,7 @@ int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
   std::vector<Job>& l4 = t_l4;
   plan.resize((size_t)n);
   l4.resize((size_t)n);
-  HookCtx ctx{mv, l2len, plan.data(), l4.data()};
+  HookCtx ctx{mv, n, l2len, plan.data(), l4.data()};
   tr.parsed();  // parsing runs inside the walk
   std::vector<uint16_t>& res = t_res;
   res.resize(2 * (size_t)n);
