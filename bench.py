@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc")
+    ap.add_argument("--scaling-ref", default=os.path.join(REPO, "profiles", "scaling_ref.json"),
+                    help="single-GPU config-4 shard rate (committed) carried in the line")
     ap.add_argument("--host-path", action="store_true",
                     help="also time H2D + kernel + D2H (host-resident rate)")
     ap.add_argument("--save-results", default=None, metavar="NPY",
@@ -289,6 +291,49 @@ def layout_floor_line(cfg: str, w, desc: str, kms) -> dict:
             "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4)}
 
 
+def gather_rank_kernels(kms, world: int, backend: str):
+    """Every rank's kernel times (mean, min, max ms per launch), gathered to
+    every rank in rank order: a (world, 3) array.  One tiny all_gather after
+    the timed region (RCCL on the GPU box, gloo in the CPU rehearsal)."""
+    import torch
+    import torch.distributed as dist
+
+    dev = "cuda" if backend == "nccl" else "cpu"
+    kms = np.asarray(kms, dtype=np.float64)
+    t = torch.tensor([kms.mean(), kms.min(), kms.max()], dtype=torch.float64, device=dev)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return np.stack([p.cpu().numpy() for p in parts])
+
+
+def rank_fields(stats, bytes_per_gpu: int, step_ms: float) -> dict:
+    """The N > 1 line's per-rank view: which GPU is the
+    slowest, and how much of a step the result gather leaves exposed."""
+    means = np.asarray(stats, dtype=np.float64)[:, 0]
+    slow = int(np.argmax(means))
+    kmax = float(means[slow])
+    return {
+        "ranks_kernel_ms": [round(float(x), 5) for x in means],
+        "kernel_ms_max_rank": round(kmax, 5),
+        "slowest_rank": slow,
+        "step_ms": round(step_ms, 4),
+        "gather_exposed_ms": round(step_ms - kmax, 4),
+        "per_gpu_gbs_min": round(bytes_per_gpu / (kmax * 1e-3) / 1e9, 1),
+    }
+
+
+def scaling_ref(path: str):
+    """The single-GPU config-4 shard rate (``bench.py --gpus 1 --config 4``)
+    from a committed profiles/ entry, so a 1 -> N efficiency can be computed
+    from like workloads (every N > 1 point is config 4; the N = 1 headline is
+    config 2).  None when the file is absent."""
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -385,22 +430,27 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
         # (profiles/r02/final/NOTES.md), hence medians.  `threads` is the box's
         # CPU share (16 per GPU): the rest of the mask belongs to the other
         # GPUs' jobs on the machine.
+        # plus every CPU of the process mask (SURVEY.md 8d "1 thread, then all
+        # host cores"; one thread per CPU, at most the harness's 256)
         outs = []
-        for nt in sorted({1, threads}):
+        n_all = min(len(allowed), 256)
+        for nt in sorted({1, threads, n_all}):
             for placement in ("pinned", "floating"):
-                rr = [timer(nt, cpus[:nt] if placement == "pinned" else None, 1)
-                      for _ in range(5)]
+                pin = (allowed[:nt] if nt > threads else cpus[:nt]) if placement == "pinned" else None
+                rr = [timer(nt, pin, 1) for _ in range(5)]
                 runs[f"{nt}_{placement}"] = float(np.median([r[0] for r in rr]))
                 spread[f"{nt}_{placement}"] = (min(r[0] for r in rr), max(r[0] for r in rr))
                 outs.append(rr[-1][1])
         best = min((k for k in runs if k.startswith(f"{threads}_")), key=runs.get)
         tn = runs[best]
         t1 = min(runs["1_pinned"], runs["1_floating"])
+        best_all = min((k for k in runs if k.startswith(f"{n_all}_")), key=runs.get)
     else:  # oracle restatement, timed the same way
         t0 = time.perf_counter(); o = port(); t1 = time.perf_counter() - t0  # noqa: E702
         outs, tn, best = [o], t1, f"{threads}_port"
         runs[best] = t1
         spread[best] = (t1, t1)
+        best_all, n_all = best, threads
     parity = bool(all(np.array_equal(o, gpu_out) for o in outs))
     rates = {k: round(gib / t, 3) for k, t in runs.items()}
     # min / max GiB/s of the 5 passes: the many-thread figure swings by 4x
@@ -423,6 +473,12 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
         "value_from": best,
         "placement": best.split("_")[1],
         "one_thread_gibs": round(gib / t1, 3),
+        # the reference on every CPU of the mask (median of 5, the faster
+        # placement); `value` stays the `cores`-thread figure (the GPU box's
+        # CPU share per GPU)
+        "all_cores_gibs": round(gib / runs[best_all], 3),
+        "all_cores_threads": n_all,
+        "all_cores_from": best_all,
         "mask_cpus": len(allowed),
         "bit_identical_to_gpu": parity,
     }
@@ -481,6 +537,13 @@ def run(args, distributed: bool, wd):
                 "packets_per_gpu": args.packets or {"4": 1 << 21, "2s": 1 << 24, "2su": 1 << 24,
                                                     "5": 131072}.get(args.config, 1 << 20),
                 "backend": os.environ.get("UINET_BENCH_BACKEND", "nccl") if distributed else None}
+        if distributed:
+            # the N > 1 line's per-rank fields, rehearsed over gloo with stand-in
+            # kernel times (rank r: 0.4 + 0.01 r ms per launch) through the same
+            # gather and arithmetic the timed run uses
+            fake = 0.4 + 0.01 * rank + np.array([0.0, -0.001, 0.001])
+            st = gather_rank_kernels(fake, plan["world"], "gloo")
+            plan["rank_fields_rehearsal"] = rank_fields(st, 3145728000, 0.45)
         print(json.dumps(plan), flush=True)
         if distributed:
             dist.barrier()
@@ -606,6 +669,7 @@ def run(args, distributed: bool, wd):
         kms = np.array([a.elapsed_time(b) for a, b in ev])  # ms, kernel only
     else:
         kms = np.array([ev[0][0].elapsed_time(ev[0][1]) / K])  # mean ms per launch
+    rank_stats = gather_rank_kernels(kms, world, backend) if distributed else None
 
     phase("parity")
     result = None
@@ -661,6 +725,12 @@ def run(args, distributed: bool, wd):
         }
         if args.config in CHAIN_CONFIGS:
             result["roofline"]["layout_floor"] = layout_floor_line(args.config, w, args.desc, kms)
+        if distributed:
+            # rank 0's kernel is the roofline above; these are every rank's
+            result["ranks"] = rank_fields(rank_stats, w["bytes"], elapsed / K * 1e3)
+        ref = scaling_ref(args.scaling_ref)
+        if ref is not None:
+            result["scaling_ref"] = ref
         if args.host_path:
             result["host_resident"] = host_path_rate(args, w)
     if world == 1 and rank == 0 and args.cpu_baseline == "auto":

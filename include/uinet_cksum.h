@@ -386,6 +386,29 @@ int uinet_cksum_multi_last_gather(void);
 int in_cksum_skip_batch_multi(const int *devices, int ndev, struct mbuf *const *m,
     const int *len, const int *skip, unsigned short *out, int n);
 
+/* ------------------------------------------------------------------------ */
+/* 2f. Host CPU accounting                                                   */
+/*                                                                          */
+/* What the host-memory entry points (2c, 2d, in_cksum_skip_batch_multi)    */
+/* cost the host: every such call adds to the CALLING thread's counters its */
+/* wall time, its own CPU time (CLOCK_THREAD_CPUTIME_ID, including any wait */
+/* for the GPU that spins) and the CPU time the engine's host-pool helper   */
+/* threads spent on it.  The per-call ABI (section 1) is not counted.       */
+/* ------------------------------------------------------------------------ */
+
+struct uinet_cksum_host_cpu {
+	uint64_t calls;          /* counted calls */
+	uint64_t packets;        /* packets / frames / headers they took */
+	uint64_t wall_ns;        /* wall time inside them */
+	uint64_t caller_cpu_ns;  /* the calling thread's CPU time inside them */
+	uint64_t helper_cpu_ns;  /* host-pool helpers' CPU time for them */
+	uint64_t device_walks;   /* calls whose mbuf chains the GPU walked */
+};
+
+/* Copies the calling thread's counters to *st (may be NULL) and, when reset
+ * is non-zero, zeroes them.  Returns UINET_CKSUM_OK. */
+int uinet_cksum_host_cpu(struct uinet_cksum_host_cpu *st, int reset);
+
 #if defined(__GNUC__)
 #pragma GCC visibility pop
 #endif

@@ -31,7 +31,7 @@ __all__ = [
     "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch", "cksum_spans", "cksum_strided",
     "cksum_chains", "pack_segments", "F_UDP", "F_NO_COMPLEMENT", "MbufChains", "MBUF_DTYPE", "MSIZE",
     "SEED_BASE", "aligned_empty", "splitmix64_bytes", "EXPORTED_SYMBOLS", "cksum_spans_multi",
-    "in_cksum_skip_batch_multi",
+    "in_cksum_skip_batch_multi", "host_cpu",
 ]
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libuinet_cksum.so")
@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "uinet_cksum_rx_offload", "uinet_cksum_tx_offload",
     "in6_cksum", "in6_cksum_pseudo", "in6_cksum_batch",
     "uinet_cksum_spans_multi", "uinet_cksum_multi_last_gather", "in_cksum_skip_batch_multi",
+    "uinet_cksum_host_cpu",
 )
 
 # Driver offload status bits (include/uinet_cksum.h section 2d).
@@ -121,6 +122,7 @@ def lib() -> ctypes.CDLL:
         "uinet_cksum_spans_multi": (_i32, [_vp, _i32, _u32, _u32, _i32, _vp]),
         "uinet_cksum_multi_last_gather": (_i32, []),
         "in_cksum_skip_batch_multi": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i32]),
+        "uinet_cksum_host_cpu": (_i32, [_vp, _i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -455,6 +457,23 @@ def in_cksum_skip_batch_multi(devices, heads, length, skip) -> np.ndarray:
     _check("in_cksum_skip_batch_multi", lib().in_cksum_skip_batch_multi(
         _ptr(devs), devs.size, _ptr(heads), _ptr(length), _ptr(skip), _ptr(out), n))
     return out
+
+
+class HostCpu(ctypes.Structure):
+    """struct uinet_cksum_host_cpu (include/uinet_cksum.h section 2f)."""
+
+    _fields_ = [("calls", _u64), ("packets", _u64), ("wall_ns", _u64), ("caller_cpu_ns", _u64),
+                ("helper_cpu_ns", _u64), ("device_walks", _u64)]
+
+
+def host_cpu(reset: bool = False) -> dict:
+    """uinet_cksum_host_cpu: this thread's host-batch counters (wall time,
+    calling-thread CPU time and host-pool helper CPU time, in ns)."""
+    st = HostCpu()
+    _check("uinet_cksum_host_cpu", lib().uinet_cksum_host_cpu(ctypes.byref(st), int(reset)))
+    d = {k: int(getattr(st, k)) for k, _ in HostCpu._fields_}
+    d["cpu_ns"] = d["caller_cpu_ns"] + d["helper_cpu_ns"]
+    return d
 
 
 def set_tuning(key: str, value: int) -> None:

@@ -64,7 +64,7 @@ void note_kernel(const void* host_stub) { t_last_kernel = host_stub; }
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_pass{2}, host_threads{8}, chains_long{128},
       chains_tile{0}, xcd_remap{1}, walk_prefetch{1}, spans_geo{0}, spans_pipe{1},
-      host_pin{0}, multi_gather{0};
+      host_pin{0}, multi_gather{0}, walk_device{1};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -87,6 +87,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v == 0 || v == 1; }},
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
+      {"walk_device", &TuningLive::walk_device, [](int v) { return v == 0 || v == 1; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -105,6 +106,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_GEO", "spans_geo"},
         {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},
         {"UINET_CKSUM_HOST_PIN", "host_pin"},          {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},
+        {"UINET_CKSUM_WALK_DEVICE", "walk_device"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -134,8 +136,40 @@ Tuning tuning() {
   x.spans_pipe = ld(t.spans_pipe);
   x.host_pin = ld(t.host_pin);
   x.multi_gather = ld(t.multi_gather);
+  x.walk_device = ld(t.walk_device);
   return x;
 }
+
+// ---- host CPU accounting (uinet_cksum_host_cpu) -----------------------------
+
+namespace {
+thread_local struct uinet_cksum_host_cpu t_cpu{};
+thread_local int t_cpu_depth = 0;
+uint64_t wall_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+}  // namespace
+
+CpuScope::CpuScope(int n) : outer(t_cpu_depth++ == 0), packets(n) {
+  if (!outer) return;
+  wall0 = wall_ns();
+  cpu0 = thread_cpu_ns();
+  helper0 = t_pool_helper_ns;
+}
+
+CpuScope::~CpuScope() {
+  --t_cpu_depth;
+  if (!outer) return;
+  t_cpu.calls++;
+  t_cpu.packets += packets > 0 ? (uint64_t)packets : 0u;
+  t_cpu.wall_ns += wall_ns() - wall0;
+  t_cpu.caller_cpu_ns += thread_cpu_ns() - cpu0;
+  t_cpu.helper_cpu_ns += t_pool_helper_ns - helper0;
+}
+
+void note_device_walk() { t_cpu.device_walks++; }
 
 namespace {
 
@@ -158,6 +192,8 @@ struct Ctx {
   uint16_t* h_out = nullptr;  // pinned results
   uint16_t* d_out = nullptr;
   size_t out_cap = 0;
+  hipEvent_t done = nullptr;  // blocking-sync event: the host sleeps while the GPU works
+  uint32_t walk_k = 0;        // device walk: segment slots per packet last needed
 };
 
 // One context per (thread, device): a thread that serves several devices --
@@ -181,14 +217,35 @@ int ctx_current(Ctx** out) {
     if (rc) return rc;
     c.device = dev;
   }
+  if (!c.done) {
+    rc = record_hip(
+        hipEventCreateWithFlags(&c.done, hipEventBlockingSync | hipEventDisableTiming));
+    if (rc) return rc;
+  }
   *out = &c;
   return UINET_CKSUM_OK;
 }
 
-// Grows the pinned staging to `bytes` (and its HBM mirror when `device`: the
-// zero-copy path reads pinned memory in place and needs none) and the result
-// buffers to `nout` entries.
-int ctx_reserve(Ctx& c, size_t bytes, size_t nout, bool device = true) {
+// Waits for everything queued on the context's stream.  A blocking-sync event
+// lets the calling thread sleep instead of polling for the whole fold (the
+// lab build -DUINET_WAIT_STREAM_SYNC polls with hipStreamSynchronize, for the
+// CPU-time A/B in DESIGN.md).
+int ctx_wait(Ctx& c) {
+#ifdef UINET_WAIT_STREAM_SYNC
+  return record_hip(hipStreamSynchronize(c.stream));
+#else
+  int rc = record_hip(hipEventRecord(c.done, c.stream));
+  if (rc) return rc;
+  return record_hip(hipEventSynchronize(c.done));
+#endif
+}
+
+// Grows the pinned staging to `bytes`, its HBM mirror to `dbytes` (default:
+// `bytes`; the zero-copy path reads pinned memory in place and passes 0) and
+// the result buffers to `nout` entries.
+int ctx_reserve(Ctx& c, size_t bytes, size_t nout, size_t dbytes = ~size_t(0)) {
+  if (dbytes == ~size_t(0)) dbytes = bytes;
+  const bool device = dbytes > 0;
   const auto grow = [](size_t cap, size_t want) {
     cap = cap ? cap : (1u << 20);
     while (cap < want) cap *= 2;
@@ -203,8 +260,8 @@ int ctx_reserve(Ctx& c, size_t bytes, size_t nout, bool device = true) {
     if (rc) return rc;
     c.h_cap = cap;
   }
-  if (device && bytes > c.d_cap) {
-    const size_t cap = grow(c.d_cap, bytes);
+  if (device && dbytes > c.d_cap) {
+    const size_t cap = grow(c.d_cap, dbytes);
     if (c.d_buf) (void)hipFree(c.d_buf);
     c.d_buf = nullptr;
     c.d_cap = 0;
@@ -421,7 +478,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   using clk = std::chrono::steady_clock;
   const clk::time_point t0 = trace ? clk::now() : clk::time_point();
   double t_walk = 0, t_desc = 0;
-  int rc = ctx_reserve(c, std::max<size_t>(c.h_cap, 1u << 20), (size_t)n, false);
+  int rc = ctx_reserve(c, std::max<size_t>(c.h_cap, 1u << 20), (size_t)n, 0);
   if (rc) return rc;
   uint64_t lo_addr = ~0ull, hi_addr = 0;
   for (const Region& r : g_regions) {
@@ -446,7 +503,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   if (rc) return rc;
   const std::vector<Region>& regs = g_regions;
   const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  const auto drain = [&]() { return record_hip(hipStreamSynchronize(c.stream)); };
+  const auto drain = [&]() { return ctx_wait(c); };
   // chunks per pipeline group: one per thread (one pool pass each; 2-64 per
   // thread lost in every A/B, profiles/r04/pruned/knobs.diff)
   const int group = std::max(1, threads);
@@ -489,7 +546,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
       if (rc) return rc;
       ring = 0;
       if (need > c.h_cap) {
-        rc = ctx_reserve(c, need * (size_t)((nch - g0 + group - 1) / group), (size_t)n, false);
+        rc = ctx_reserve(c, need * (size_t)((nch - g0 + group - 1) / group), (size_t)n, 0);
         if (rc) return rc;
         rc = record_hip(hipHostGetDevicePointer(&dbuf, c.h_buf, 0));
         if (rc) return rc;
@@ -570,6 +627,140 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   return UINET_CKSUM_OK;
 }
 
+// ---- device walk (cksum_walk.hip) -------------------------------------------
+//
+// Registered memory and a chain-walking batch: the host writes only the jobs
+// (head, len, skip, seed: 20 B per packet) into pinned memory; the GPU walks
+// the chains (k_walk_mbufs) into a K-slot segment list in HBM and folds it with
+// the chain kernel, reading mbuf headers and packet bytes in place over PCIe.
+// The host thread sleeps on a blocking-sync event meanwhile.
+
+enum WalkKind { kWalkNone = 0, kWalkSkip = 1, kWalkPseudo = 2 };
+constexpr uint32_t kWalkKMax = 4096;  // longer chains take the host walk
+
+// job(i) -> Job (the in_cksum_skip form; len and skip as the caller gave
+// them).  Returns kFallback (nothing delivered) when the batch must take the
+// host walk.  Called with g_reg_mu held (shared) and at least one region.
+template <typename JobFn>
+int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32_t flags,
+                      WalkKind kind, bool seeded, const JobFn& job, uint16_t* out16,
+                      unsigned* out32, bool trace) {
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = trace ? clk::now() : clk::time_point();
+  const size_t nreg = g_regions.size();
+  if (nreg == 0 || nreg > (size_t)kWalkRegionsMax) return kFallback;
+  uint64_t lo_addr = ~0ull;
+  for (const Region& r : g_regions) lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
+  uint32_t K = c.walk_k ? c.walk_k : 4;
+  const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const size_t N = (size_t)n;
+  // pinned: heads u64 | len i32 | skip i32 | seed u32 | regions | status u32[2]
+  const size_t h_len = a16(8 * N), h_skip = h_len + a16(4 * N), h_seed = h_skip + a16(4 * N);
+  const size_t h_reg = h_seed + (seeded ? a16(4 * N) : 0);
+  const size_t h_st = h_reg + a16(sizeof(WalkRegionHost) * nreg), h_end = h_st + 16;
+  // HBM: seg_off u64[n K] | seg_len u32[n K] | pkt_seg u32[n + 1] | len | skip | seed | status
+  const auto dev_layout = [&](uint32_t k, size_t* o_sl, size_t* o_ps, size_t* o_ln, size_t* o_sk,
+                              size_t* o_sd, size_t* o_st) {
+    *o_sl = a16(8 * N * k);
+    *o_ps = *o_sl + a16(4 * N * k);
+    *o_ln = *o_ps + a16(4 * (N + 1));
+    *o_sk = *o_ln + a16(4 * N);
+    *o_sd = *o_sk + a16(4 * N);
+    *o_st = *o_sd + a16(4 * N);
+    return *o_st + 16;
+  };
+  size_t d_sl, d_ps, d_ln, d_sk, d_sd, d_st;
+  int rc = ctx_reserve(c, h_end, N, dev_layout(K, &d_sl, &d_ps, &d_ln, &d_sk, &d_sd, &d_st));
+  if (rc) return rc;
+  uint8_t* h = c.h_buf;
+  uint64_t* heads = reinterpret_cast<uint64_t*>(h);
+  int32_t* jl = reinterpret_cast<int32_t*>(h + h_len);
+  int32_t* js = reinterpret_cast<int32_t*>(h + h_skip);
+  uint32_t* jd = reinterpret_cast<uint32_t*>(h + h_seed);
+  // the jobs, in chunks of consecutive packets on the host pool (a hook's
+  // jobs are made -- its headers parsed -- here)
+  const int nch = (n + cs - 1) / cs;
+  pool.run(nch, threads, [&](int j) {
+    const int i1 = std::min(n, (j + 1) * cs);
+    for (int i = j * cs; i < i1; i++) {
+      const Job J = job(i);
+      heads[i] = reinterpret_cast<uint64_t>(J.m);
+      jl[i] = J.len;
+      js[i] = J.skip;
+      if (seeded) jd[i] = J.seed;
+    }
+  }, tuning().host_pin != 0);
+  WalkRegionHost* R = reinterpret_cast<WalkRegionHost*>(h + h_reg);
+  for (size_t k = 0; k < nreg; k++)
+    R[k] = WalkRegionHost{g_regions[k].base, g_regions[k].end, (int64_t)g_regions[k].delta};
+  const clk::time_point t1 = trace ? clk::now() : clk::time_point();
+  void* dh = nullptr;
+  rc = record_hip(hipHostGetDevicePointer(&dh, c.h_buf, 0));
+  if (rc) return rc;
+  void* dout = nullptr;
+  rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
+  if (rc) return rc;
+  const uint8_t* dj = static_cast<const uint8_t*>(dh);
+  volatile uint32_t* st = reinterpret_cast<volatile uint32_t*>(h + h_st);
+  for (int attempt = 0; attempt < 2; attempt++) {
+    rc = ctx_reserve(c, h_end, N, dev_layout(K, &d_sl, &d_ps, &d_ln, &d_sk, &d_sd, &d_st));
+    if (rc) return rc;
+    uint8_t* d = c.d_buf;
+    rc = record_hip(hipMemsetAsync(d + d_st, 0, 8, c.stream));
+    if (rc) return rc;
+    rc = launch_walk_mbufs(reinterpret_cast<const uint64_t*>(dj),
+                           reinterpret_cast<const int32_t*>(dj + h_len),
+                           reinterpret_cast<const int32_t*>(dj + h_skip),
+                           seeded ? reinterpret_cast<const uint32_t*>(dj + h_seed) : nullptr,
+                           reinterpret_cast<const WalkRegionHost*>(dj + h_reg), (int)nreg,
+                           (uint32_t)n, K, lo_addr, kind == kWalkPseudo,
+                           reinterpret_cast<uint64_t*>(d), reinterpret_cast<uint32_t*>(d + d_sl),
+                           reinterpret_cast<uint32_t*>(d + d_ps),
+                           reinterpret_cast<uint32_t*>(d + d_ln),
+                           reinterpret_cast<uint32_t*>(d + d_sk),
+                           reinterpret_cast<uint32_t*>(d + d_sd),
+                           reinterpret_cast<uint32_t*>(d + d_st), c.stream);
+    if (!rc)
+      rc = launch_chains(reinterpret_cast<const void*>(lo_addr),
+                         reinterpret_cast<const uint64_t*>(d),
+                         reinterpret_cast<const uint32_t*>(d + d_sl),
+                         reinterpret_cast<const uint32_t*>(d + d_ps),
+                         reinterpret_cast<const uint32_t*>(d + d_ln),
+                         reinterpret_cast<const uint32_t*>(d + d_sk),
+                         seeded ? reinterpret_cast<const uint32_t*>(d + d_sd) : nullptr,
+                         static_cast<uint16_t*>(dout), (uint32_t)n, flags, 0, c.stream);
+    if (!rc)
+      rc = record_hip(hipMemcpyAsync(h + h_st, d + d_st, 8, hipMemcpyDeviceToHost, c.stream));
+    const int wrc = ctx_wait(c);
+    if (rc) return rc;
+    if (wrc) return wrc;
+    if (st[0]) return kFallback;  // a job the host walk must take
+    const uint32_t longest = st[1];
+    // the next batch on this thread starts from this one's longest chain
+    uint32_t k2 = 4;
+    while (k2 < longest) k2 *= 2;
+    c.walk_k = k2;
+    if (longest <= K) {
+      for (int i = 0; i < n; i++) {
+        if (out16) out16[i] = c.h_out[i];
+        if (out32) out32[i] = c.h_out[i];
+      }
+      note_device_walk();
+      if (trace)
+        fprintf(stderr,
+                "uinet_cksum host batch: n=%d device walk K=%u longest=%u | jobs %.3f fold "
+                "%.3f total %.3f ms\n",
+                n, K, longest, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(clk::now() - t1).count(),
+                std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+      return UINET_CKSUM_OK;
+    }
+    if (k2 > kWalkKMax || (uint64_t)N * k2 > 0xffffffffull) return kFallback;
+    K = k2;  // a chain longer than K: walk again with room for it
+  }
+  return kFallback;
+}
+
 struct ChainRef {
   const MbufHdr* m;  // first mbuf, nullptr = nothing to chase
   long limit;        // bytes from the chain start the walk consumes
@@ -598,9 +789,11 @@ inline void prefetch_ahead(const ChainRef& r, int depth) {
 // `head(i)` is the ChainRef the walk will follow, {nullptr, 0} for none),
 // then fold the pieces in place (all registered, even start parity; pipelined
 // with the walk) or pack them into pinned staging.
-template <typename WalkFn, typename HeadFn>
+// `job(i)` is packet i in the in_cksum_skip form (head, len, skip, seed) for
+// the device walk; `kind` kWalkNone keeps the batch on the host walk.
+template <typename WalkFn, typename HeadFn, typename JobFn>
 int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, WalkFn walk,
-                   HeadFn head) {
+                   HeadFn head, WalkKind kind, bool seeded, JobFn job) {
   if (n < 0) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
   Ctx* cp = nullptr;
@@ -669,6 +862,11 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   // whole batch down the staging path below.
   {
     std::shared_lock<std::shared_mutex> g(g_reg_mu);
+    if (!g_regions.empty() && kind != kWalkNone && tuning().walk_device) {
+      rc = device_walk_batch(c, pool, threads, cs, n, flags, kind, seeded, job, out16, out32,
+                             trace);
+      if (rc != kFallback) return rc;
+    }
     if (!g_regions.empty()) {
       rc = zero_copy_batch(c, B, pool, threads, nch, n, flags, walk_chunk, trace);
       if (rc != kFallback) {
@@ -780,7 +978,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     }
   }
   if (trace) t_launch = clk::now();
-  rc = record_hip(hipStreamSynchronize(c.stream));
+  rc = ctx_wait(c);
   if (rc) return rc;
   if (trace) {
     const auto ms = [](clk::time_point a, clk::time_point b) {
@@ -808,7 +1006,8 @@ int run_jobs(const Job* jobs, int n, uint16_t* out) {
   return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
     w.walk_skip(jobs[i].m, jobs[i].len, jobs[i].skip);
     return jobs[i].seed;
-  }, [&](int i) { return ChainRef{jobs[i].m, (long)jobs[i].len}; });
+  }, [&](int i) { return ChainRef{jobs[i].m, (long)jobs[i].len}; }, kWalkSkip, true,
+     [&](int i) { return jobs[i]; });
 }
 
 int run_jobs_made(int n, JobMaker make, JobFirst first, void* ctx, uint16_t* out) {
@@ -817,7 +1016,8 @@ int run_jobs_made(int n, JobMaker make, JobFirst first, void* ctx, uint16_t* out
     const Job j = make(ctx, i);
     w.walk_skip(j.m, j.len, j.skip);
     return j.seed;
-  }, [&](int i) { return ChainRef{first(ctx, i), 0x7fffffffL}; });  // chased like a whole chain
+  }, [&](int i) { return ChainRef{first(ctx, i), 0x7fffffffL}; },  // chased like a whole chain
+     kWalkSkip, true, [&](int i) { return make(ctx, i); });
 }
 
 namespace {
@@ -918,6 +1118,12 @@ int uinet_cksum_unregister_host(void* base) {
   return UINET_CKSUM_EINVAL;
 }
 
+int uinet_cksum_host_cpu(struct uinet_cksum_host_cpu* st, int reset) {
+  if (st) *st = t_cpu;
+  if (reset) t_cpu = {};
+  return UINET_CKSUM_OK;
+}
+
 int uinet_cksum_set_tuning(const char* key, int value) {
   if (!key) return UINET_CKSUM_EINVAL;
   std::atomic<int>* f = tuning_field(tuning_live(), key, value);
@@ -993,10 +1199,13 @@ int uinet_cksum_chains32(const void* base, const uint32_t* seg_off, const uint16
 int in_cksum_skip_batch(struct mbuf* const* m, const int* len, const int* skip,
                         unsigned short* out, int n) {
   if (n > 0 && (!m || !len || !skip || !out)) return UINET_CKSUM_EINVAL;
+  CpuScope cpu(n);
   return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
     w.walk_skip(reinterpret_cast<const MbufHdr*>(m[i]), len[i], skip[i]);
     return 0u;
-  }, [&](int i) { return ChainRef{reinterpret_cast<const MbufHdr*>(m[i]), (long)len[i]}; });
+  }, [&](int i) { return ChainRef{reinterpret_cast<const MbufHdr*>(m[i]), (long)len[i]}; },
+     kWalkSkip, false,
+     [&](int i) { return Job{reinterpret_cast<const MbufHdr*>(m[i]), len[i], skip[i], 0u}; });
 }
 
 int in_cksum_pseudo_header_batch(struct mbuf* const* m, const int* plen, const int* off0,
@@ -1004,6 +1213,7 @@ int in_cksum_pseudo_header_batch(struct mbuf* const* m, const int* plen, const i
                                  const uint8_t* protonum, uint16_t* out, int n) {
   if (n > 0 && (!m || !plen || !off0 || !src || !dst || !protonum || !out))
     return UINET_CKSUM_EINVAL;
+  CpuScope cpu(n);
   return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
     w.walk_pseudo(reinterpret_cast<const MbufHdr*>(m[i]), plen[i], off0[i]);
     // in_cksum.c:252-253; folded on the host so it fits the u32 seed slot
@@ -1013,6 +1223,15 @@ int in_cksum_pseudo_header_batch(struct mbuf* const* m, const int* plen, const i
     return fold16_host(s);
   }, [&](int i) {
     return ChainRef{reinterpret_cast<const MbufHdr*>(m[i]), (long)off0[i] + plen[i]};
+  }, kWalkPseudo, true, [&](int i) {
+    // in_cksum_skip(m, off0 + plen, off0) when off0 lies in the first mbuf
+    // (the walk checks that); an off0 + plen past INT_MAX takes the host walk
+    // (a negative skip is the walk's "host" mark)
+    const long e = (long)off0[i] + plen[i];
+    const uint64_t s = (uint64_t)src[i] + dst[i] + bswap16(protonum[i]) +
+                       bswap16((uint16_t)plen[i]);
+    return Job{reinterpret_cast<const MbufHdr*>(m[i]), e > 0x7fffffffL ? 0 : (int)e,
+               e > 0x7fffffffL ? -1 : off0[i], fold16_host(s)};
   });
 }
 
@@ -1021,6 +1240,7 @@ int in6_cksum_batch(struct mbuf* const* m, const uint8_t* nxt, const uint32_t* o
   if (n > 0 && (!m || !nxt || !off || !len || !out)) return UINET_CKSUM_EINVAL;
   for (int i = 0; i < n; i++)  // the header is read on the host; off + len fits an int
     if (!m[i] || (uint64_t)off[i] + len[i] > 0x7fffffffull) return UINET_CKSUM_EINVAL;
+  CpuScope cpu(n);
   return run_host_batch(n, 0, out, nullptr, [&](int i, PacketWalk& w) -> uint32_t {
     // in6_cksum.c:208-350: off counts from the chain start, then len bytes
     const MbufHdr* mm = reinterpret_cast<const MbufHdr*>(m[i]);
@@ -1028,11 +1248,15 @@ int in6_cksum_batch(struct mbuf* const* m, const uint8_t* nxt, const uint32_t* o
     return in6_pseudo_fold(mm->m_data, len[i], nxt[i]);  // "contiguous IP6 header"
   }, [&](int i) {
     return ChainRef{reinterpret_cast<const MbufHdr*>(m[i]), (long)off[i] + (long)len[i]};
+  }, kWalkSkip, true, [&](int i) {
+    const MbufHdr* mm = reinterpret_cast<const MbufHdr*>(m[i]);
+    return Job{mm, (int)(off[i] + len[i]), (int)off[i], in6_pseudo_fold(mm->m_data, len[i], nxt[i])};
   });
 }
 
 int in_cksum_hdr_batch(const struct ip* const* ip, unsigned int* out, int n) {
   if (n > 0 && (!ip || !out)) return UINET_CKSUM_EINVAL;
+  CpuScope cpu(n);
   return run_host_batch(n, 0, nullptr, out, [&](int i, PacketWalk& w) -> uint32_t {
     // in_cksum.c:278-285: in_cksumdata(ip, 20) weights by ADDRESS parity and
     // never re-aligns, so the header's logical start parity is its address
@@ -1041,7 +1265,8 @@ int in_cksum_hdr_batch(const struct ip* const* ip, unsigned int* out, int n) {
     w.clen = (long)(reinterpret_cast<uintptr_t>(ip[i]) & 1);
     w.take(reinterpret_cast<const uint8_t*>(ip[i]), 20);
     return 0u;
-  }, [](int) { return ChainRef{nullptr, 0}; });
+  }, [](int) { return ChainRef{nullptr, 0}; }, kWalkNone, false,
+     [](int) { return Job{nullptr, 0, 0, 0u}; });
 }
 
 // ---- drop-in per-call ABI (sys/amd64/include/in_cksum.h:76-83) --------------

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "uinet_cksum.h"
+#include "walk_xlate.h"
 
 namespace uinet {
 
@@ -27,6 +28,8 @@ struct Tuning {
   int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead
   int host_pin;        // host pool helpers pinned to CPUs 1.. of the process mask (0/1)
   int multi_gather;    // uinet_cksum_spans_multi: 0 RCCL gather when it applies, 1 peer copies
+  int walk_device;     // host-mbuf batches in registered memory: 1 the GPU walks the chains
+                       // (cksum_walk.hip), 0 the host walks them
 };
 Tuning tuning();
 // True when G * 16 + U names a compiled span-kernel geometry.
@@ -87,5 +90,23 @@ int launch_chains32(const void* base, const uint32_t* seg_off, const uint16_t* s
                     const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                     const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
                     uint32_t len_hint, hipStream_t stream);
+
+// Device-side chain walk (cksum_walk.hip) for host-mbuf batches whose mbufs
+// and bytes lie in registered host memory.  Host range [base, end) is read by
+// the device at host address + delta; regions sorted by base.
+constexpr int kWalkRegionsMax = 256;
+constexpr uint32_t kWalkFallback = 1;  // status[0]: a job the host walk must take
+constexpr uint32_t kWalkUnmapped = 2;  // status[0]: a pointer outside the regions
+// Packet i's chain (heads[i], len[i], skip[i], seed[i]; seed may be NULL) into
+// row i of a K-slot segment list in HBM (seg_off relative to lo_dev; pkt_seg
+// = i * K), plus u32 len / skip / seed arrays for launch_chains.  status (2 u32
+// in device memory, zeroed by the caller): [0] kWalk* bits, [1] the longest
+// chain when one exceeds K.  `pseudo`: the in_cksum_pseudo_header form (skip
+// = off0 must lie within the first mbuf).
+int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* skip,
+                      const uint32_t* seed, const WalkRegionHost* regions, int nreg, uint32_t n,
+                      uint32_t K, uint64_t lo_dev, bool pseudo, uint64_t* seg_off,
+                      uint32_t* seg_len, uint32_t* pkt_seg, uint32_t* len_out, uint32_t* skip_out,
+                      uint32_t* seed_out, uint32_t* status, hipStream_t stream);
 
 }  // namespace uinet

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "cksum_internal.h"
+#include "host_batch.h"
 #include "host_pool.h"
 
 namespace uinet {
@@ -333,6 +334,7 @@ int in_cksum_skip_batch_multi(const int* devices, int ndev, struct mbuf* const* 
                               const int* skip, unsigned short* out, int n) {
   if (ndev <= 0 || !devices || n < 0) return UINET_CKSUM_EINVAL;
   if (n > 0 && (!m || !len || !skip || !out)) return UINET_CKSUM_EINVAL;
+  CpuScope cpu(n);
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return UINET_CKSUM_ENODEV;
   for (int j = 0; j < ndev; j++)

@@ -458,6 +458,7 @@ extern "C" {
 int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
   if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
+  CpuScope cpu(n);
   PhaseTrace tr("rx");
   std::vector<RxPlan>& plan = t_rx;
   std::vector<Job>& l4 = t_l4;
@@ -499,6 +500,7 @@ int uinet_cksum_rx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* st
 int uinet_cksum_tx_offload(struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
   if (n < 0 || (n > 0 && !mv) || l2len < -1) return UINET_CKSUM_EINVAL;
   if (n == 0) return UINET_CKSUM_OK;
+  CpuScope cpu(n);
   PhaseTrace tr("tx");
   std::vector<TxPlan>& plan = t_tx;
   std::vector<Job>& l4 = t_l4;

@@ -1,0 +1,134 @@
+// MI355X (gfx950) device-side mbuf chain walk for host-mbuf batches whose
+// mbufs and packet bytes all lie in registered host memory
+// (uinet_cksum_register_host: the UMA slabs of uinet_vm_kern.c:48-51, the
+// netmap rings of uinet_if_netmap_host.c:153).
+//
+// The host hands over only the batch's jobs -- head mbuf pointer, len, skip,
+// seed per packet -- and the small table of registered regions.  One lane
+// per packet chases m_next / m_data / m_len (struct m_hdr offsets 0 / 16 /
+// 24, /root/reference/sys/sys/mbuf.h:90-98) over PCIe through the regions'
+// device aliases, exactly as far as in_cksum_skip reads the chain
+// (/root/reference/sys/amd64/amd64/in_cksum.c:203-229: until `len` bytes
+// from the chain start are covered or m_next is NULL), and writes one
+// segment per mbuf into the packet's K-slot row of an HBM segment list
+// (zero-length slots pad the row).  k_chains_pipe then folds that list with
+// the packets' own len / skip -- the [skip, len) clip, zero-length mbufs and
+// the logical parity are the chain kernel's, which is parity-tested against
+// the oracle -- reading the packet bytes in place over PCIe.
+//
+// Anything the walk cannot take the way the host walk would is reported in
+// the status word and the host runs that batch through its own walk instead:
+// a pointer outside the registered regions, a negative m_len or skip, and (in
+// the in_cksum_pseudo_header form) a first mbuf shorter than off0, where the
+// reference's sum is not the skip form's (in_cksum.c:254-256).  status[1] is
+// the longest chain: when it exceeds K the batch is walked again with room
+// for it, and the next batch starts from it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cksum_internal.h"
+#include "walk_xlate.h"
+
+namespace uinet {
+namespace {
+
+using WalkRegion = WalkRegionHost;
+
+__global__ __launch_bounds__(256) void k_walk_mbufs(
+    const uint64_t* __restrict__ heads, const int32_t* __restrict__ jlen,
+    const int32_t* __restrict__ jskip, const uint32_t* __restrict__ jseed,
+    const WalkRegion* __restrict__ regions, int nreg, uint32_t n, uint32_t K, uint64_t lo_dev,
+    int pseudo, uint64_t* __restrict__ seg_off, uint32_t* __restrict__ seg_len,
+    uint32_t* __restrict__ pkt_seg, uint32_t* __restrict__ len_out,
+    uint32_t* __restrict__ skip_out, uint32_t* __restrict__ seed_out,
+    uint32_t* __restrict__ status) {
+  __shared__ WalkRegion R[kWalkRegionsMax];
+  for (int k = (int)threadIdx.x; k < nreg; k += (int)blockDim.x) R[k] = regions[k];
+  __syncthreads();
+  const uint32_t stride = gridDim.x * blockDim.x;
+  uint32_t any_bad = 0, longest = 0;  // this lane's, over its packets
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t head = heads[i];
+    const int32_t L = jlen[i], S = jskip[i];
+    const uint32_t lim = L < 0 ? 0u : (uint32_t)L;  // len < 0: nothing is summed
+    uint32_t bad = S < 0 ? kWalkFallback : 0u;
+    uint32_t cnt = 0;
+    uint64_t cum = 0;
+    const size_t row = (size_t)i * K;
+    for (uint64_t m = head; !bad && m && cum < lim;) {
+      uint64_t dm;
+      if (!walk_xlate(R, nreg, m, 32, &dm)) {
+        bad = kWalkUnmapped;
+        break;
+      }
+      const uint64_t* h = reinterpret_cast<const uint64_t*>(dm);
+      const uint64_t next = h[0];
+      const uint64_t data = h[2];
+      const int32_t ml = reinterpret_cast<const int32_t*>(dm)[6];
+      if (ml < 0 || (pseudo && cnt == 0 && ml < S)) {
+        bad = kWalkFallback;
+        break;
+      }
+      uint64_t off = 0;
+      if (ml > 0) {
+        uint64_t dd;
+        if (!walk_xlate(R, nreg, data, (uint64_t)ml, &dd)) {
+          bad = kWalkUnmapped;
+          break;
+        }
+        off = dd - lo_dev;
+      }
+      if (cnt < K) {
+        seg_off[row + cnt] = off;
+        seg_len[row + cnt] = (uint32_t)ml;
+      }
+      cnt++;
+      cum += (uint64_t)ml;
+      m = next;
+    }
+    for (uint32_t k = cnt; k < K; k++) {
+      seg_off[row + k] = 0;
+      seg_len[row + k] = 0;
+    }
+    any_bad |= bad;
+    longest = max(longest, cnt);
+    pkt_seg[i] = i * K;
+    if (i == n - 1) pkt_seg[n] = n * K;
+    len_out[i] = lim;
+    skip_out[i] = (uint32_t)S;
+    seed_out[i] = jseed ? jseed[i] : 0u;
+  }
+  // one atomic per wave: the status bits and the longest chain (the host
+  // sizes the next batch's rows by it)
+  for (int d = 32; d; d >>= 1) {
+    any_bad |= (uint32_t)__shfl_xor((int)any_bad, d);
+    longest = max(longest, (uint32_t)__shfl_xor((int)longest, d));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (any_bad) atomicOr(&status[0], any_bad);
+    if (longest) atomicMax(&status[1], longest);
+  }
+}
+
+}  // namespace
+
+int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* skip,
+                      const uint32_t* seed, const WalkRegionHost* regions, int nreg, uint32_t n,
+                      uint32_t K, uint64_t lo_dev, bool pseudo, uint64_t* seg_off,
+                      uint32_t* seg_len, uint32_t* pkt_seg, uint32_t* len_out, uint32_t* skip_out,
+                      uint32_t* seed_out, uint32_t* status, hipStream_t stream) {
+  if (n == 0) return UINET_CKSUM_OK;
+  if (nreg < 1 || nreg > kWalkRegionsMax || K == 0 || (uint64_t)n * K > 0xffffffffull)
+    return UINET_CKSUM_EINVAL;
+  // one lane per packet, every chain in flight at once: the walk is a chase of
+  // dependent PCIe reads, so its time is hops x latency when the grid covers
+  // the batch (256 CUs x 2048 lanes)
+  const uint64_t blocks64 = ((uint64_t)n + 255) / 256;
+  const int blocks = (int)(blocks64 < 8192 ? blocks64 : 8192);
+  UINET_LAUNCH(k_walk_mbufs, dim3(blocks), dim3(256), 0, stream, heads, len, skip, seed,
+               regions, nreg, n, K, lo_dev, pseudo ? 1 : 0,
+               seg_off, seg_len, pkt_seg, len_out, skip_out, seed_out, status);
+  return check_launch();
+}
+
+}  // namespace uinet

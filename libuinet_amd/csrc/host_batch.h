@@ -69,6 +69,22 @@ typedef Job (*JobMaker)(void* ctx, int i);
 typedef const MbufHdr* (*JobFirst)(void* ctx, int i);
 int run_jobs_made(int n, JobMaker make, JobFirst first, void* ctx, uint16_t* out);
 
+// Host CPU accounting of the batch entry points (uinet_cksum_host_cpu): a
+// CpuScope at each public host-batch entry adds the call's wall time, the
+// calling thread's CPU time and the pool helpers' CPU time to the calling
+// thread's counters.  Nested scopes (a hook's batch) count once.
+struct CpuScope {
+  explicit CpuScope(int packets);
+  ~CpuScope();
+  CpuScope(const CpuScope&) = delete;
+  CpuScope& operator=(const CpuScope&) = delete;
+  bool outer;
+  int packets;
+  uint64_t wall0, cpu0, helper0;
+};
+// The calling thread's batch was walked on the device (counted by the scope).
+void note_device_walk();
+
 // The per-call ABI's host fold (cksum_percall.cpp): one chain on the calling
 // thread, no device involved, no error path (like the reference).
 uint16_t host_cksum_skip(const MbufHdr* m, long len, long skip, uint32_t seed);

@@ -10,6 +10,8 @@
 
 #include <pthread.h>
 #include <sched.h>
+#include <stdint.h>
+#include <time.h>
 
 #include <atomic>
 #include <condition_variable>
@@ -19,6 +21,18 @@
 #include <vector>
 
 namespace uinet {
+
+// CPU time of the calling thread (CLOCK_THREAD_CPUTIME_ID), nanoseconds.
+inline uint64_t thread_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+// CPU time that pool helpers spent on this thread's pool runs (and, nested,
+// on the runs those helpers made): uinet_cksum_host_cpu adds it to the
+// calling thread's own CPU time.
+inline thread_local uint64_t t_pool_helper_ns = 0;
 
 class HostPool {
  public:
@@ -49,6 +63,8 @@ class HostPool {
     std::unique_lock<std::mutex> g(mu_);
     done_.wait(g, [&] { return pending_ == 0; });
     fn_ = nullptr;
+    t_pool_helper_ns += helper_ns_;
+    helper_ns_ = 0;
   }
 
  private:
@@ -90,8 +106,13 @@ class HostPool {
         }
         if (pthread_setaffinity_np(pthread_self(), sizeof(set), &set) == 0) pinned = pin;
       }
+      // this helper's CPU time for the run, including what helpers of runs
+      // it made itself spent (a multi-device shard's own walk pool)
+      const uint64_t c0 = thread_cpu_ns() + t_pool_helper_ns;
       drain();
+      const uint64_t c1 = thread_cpu_ns() + t_pool_helper_ns;
       std::lock_guard<std::mutex> g(mu_);
+      helper_ns_ += c1 - c0;
       if (--pending_ == 0) done_.notify_one();
     }
   }
@@ -103,6 +124,7 @@ class HostPool {
   const std::function<void(int)>* fn_ = nullptr;
   std::atomic<int> next_{0};
   int jobs_ = 0, helpers_ = 0, pending_ = 0;
+  uint64_t helper_ns_ = 0;  // helpers' CPU time in the current run (under mu_)
   bool pin_ = false;
   uint64_t gen_ = 0;
 };

@@ -75,7 +75,10 @@ class MbufChains:
         self.seg_len = seg_len
         self.pkt_seg = pkt_seg
         nseg = seg_off.size
-        self.mbufs = np.zeros(max(nseg, 1), dtype=MBUF_DTYPE)
+        # page-aligned records (zeroed), so the mbufs can be registered with
+        # the engine (uinet_cksum_register_host) as a region of their own, as
+        # libuinet's UMA slabs are (the device walk reads them in place)
+        self.mbufs = aligned_empty(max(nseg, 1) * MSIZE).view(MBUF_DTYPE)
         base = self.mbufs.ctypes.data
         addr = base + MSIZE * np.arange(nseg, dtype=np.uint64)
         nxt = addr + np.uint64(MSIZE)

@@ -75,6 +75,14 @@ def test_bench_gpus2_config4_full_shard_gloo(tmp_path, torch_dev):
     assert d["bit_identical"] is True and d["parity"]["packets"] == 2 * 2097152
     assert d["config"]["workload"].startswith("config4: 4,194,304 x 1500 B")
     assert d["config"]["packets_per_gpu"] == 2097152
+    # every rank's kernel, not only rank 0's
+    rk = d["ranks"]
+    assert len(rk["ranks_kernel_ms"]) == 2 and all(x > 0 for x in rk["ranks_kernel_ms"])
+    assert rk["kernel_ms_max_rank"] == max(rk["ranks_kernel_ms"])
+    assert rk["slowest_rank"] in (0, 1)
+    assert rk["step_ms"] == round(d["ms_per_step"], 4)
+    assert abs(rk["gather_exposed_ms"] - (rk["step_ms"] - rk["kernel_ms_max_rank"])) < 1e-3
+    assert rk["per_gpu_gbs_min"] > 0
     got = np.load(path)
     assert got.dtype == np.uint16 and got.size == 2 * 2097152
     np.testing.assert_array_equal(got, _want_config2(2097152, 2))

@@ -23,7 +23,15 @@ def _run(args, env_extra=None, timeout=180):
 
 
 def _plans(stdout):
-    return [json.loads(m) for m in re.findall(r"\{[^{}]*\"rank\"[^{}]*\}", stdout)]
+    """Every rank's plan object (ranks share the launcher's stdout, so two
+    lines may run together)."""
+    dec = json.JSONDecoder()
+    out, i = [], stdout.find('{"rank"')
+    while i >= 0:
+        obj, end = dec.raw_decode(stdout, i)
+        out.append(obj)
+        i = stdout.find('{"rank"', end)
+    return out
 
 
 def test_world_size_mismatch_is_an_error():
@@ -51,6 +59,24 @@ def test_gpus_n_spawns_n_ranks_with_config4_default():
     assert {p["world"] for p in plans} == {3}
     assert {p["config"] for p in plans} == {"4"}
     assert {p["packets_per_gpu"] for p in plans} == {2097152}
+
+
+def test_rank_fields_gathered_over_gloo():
+    """The N > 1 line's per-rank fields (ranks_kernel_ms, kernel_ms_max_rank,
+    slowest_rank, step_ms, gather_exposed_ms, per_gpu_gbs_min) come from one
+    all_gather of every rank's kernel times: rehearsed at world 2 over gloo
+    with stand-in times (rank r: 0.4 + 0.01 r ms)."""
+    r = _run(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    plans = _plans(r.stdout)
+    assert len(plans) == 2
+    for p in plans:
+        f = p["rank_fields_rehearsal"]
+        assert f["ranks_kernel_ms"] == [0.4, 0.41]
+        assert f["kernel_ms_max_rank"] == 0.41 and f["slowest_rank"] == 1
+        assert f["step_ms"] == 0.45 and f["gather_exposed_ms"] == 0.04
+        assert f["per_gpu_gbs_min"] == round(3145728000 / 0.41e-3 / 1e9, 1)
+
 
 
 def test_single_gpu_default_is_config2_without_launcher():

@@ -1,0 +1,196 @@
+"""The device-side chain walk (csrc/cksum_walk.hip): host-mbuf batches whose
+mbufs and packet bytes all lie in registered host memory are walked by the
+GPU (m_next / m_data / m_len read over PCIe) and folded by the chain kernel.
+Every case is checked bit-exact against the oracle, and
+uinet_cksum_host_cpu().device_walks says whether the GPU walked the batch or
+the host walk took it (a pointer outside the regions, a pseudo-header off0
+past the first mbuf, a chain longer than the walk takes)."""
+from __future__ import annotations
+
+import contextlib
+
+import numpy as np
+import pytest
+
+import libuinet_amd as u
+from libuinet_amd.mbuf import MbufChains
+
+from test_gpu_parity import rand_arena
+
+pytestmark = pytest.mark.gpu
+
+
+@contextlib.contextmanager
+def registered(*bufs):
+    for b in bufs:
+        u.register_host(b)
+    try:
+        yield
+    finally:
+        for b in bufs:
+            u.unregister_host(b)
+
+
+def walks(fn):
+    """(result, device walks during fn())."""
+    before = u.host_cpu()["device_walks"]
+    r = fn()
+    return r, u.host_cpu()["device_walks"] - before
+
+
+def chains(rng, arena, n, max_seg=12, max_len=300, zero_frac=0.1):
+    nseg = rng.integers(1, max_seg + 1, n)
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = rng.integers(0, max_len + 1, s)
+    seg_len[rng.random(s) < zero_frac] = 0
+    seg_off = rng.integers(0, arena.size - max_len - 1, s).astype(np.int64)
+    return MbufChains(arena, seg_off, seg_len, pkt_seg), seg_len, pkt_seg
+
+
+@pytest.fixture(scope="module")
+def arena(torch_dev):
+    return rand_arena(4 << 20, 777)
+
+
+def test_device_walk_skip_batch_edges(ora, arena):
+    """Zero-length mbufs, skip exactly on an mbuf boundary, len beyond the
+    chain, len < skip, len 0, single-mbuf and long chains."""
+    rng = np.random.default_rng(1)
+    n = 4096
+    ch, seg_len, pkt_seg = chains(rng, arena, n)
+    cs = np.concatenate([[0], np.cumsum(seg_len)])
+    tot = cs[pkt_seg[1:]] - cs[pkt_seg[:-1]]
+    length = tot.copy()
+    skip = np.zeros(n, np.int64)
+    k = np.arange(n) % 8
+    # skip on the first mbuf boundary
+    first_end = seg_len[pkt_seg[:-1]]
+    skip[k == 1] = first_end[k == 1]
+    length[k == 2] = tot[k == 2] + 100       # len beyond the chain
+    length[k == 3] = 0
+    skip[k == 4] = 20
+    length[k == 4] = 10                      # len < skip
+    skip[k == 5] = np.minimum(tot[k == 5], 41)
+    length[k == 6] = np.maximum(0, tot[k == 6] - 7)
+    skip[k == 7] = tot[k == 7]               # skip == whole chain
+    with registered(arena, ch.mbufs):
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, length, skip))
+    assert nw == 1, "the GPU did not walk this batch"
+    want = ora.skip_batch(ch.heads, length, skip)
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+
+
+def test_device_walk_long_chains_grow_rows(ora, arena):
+    """Chains longer than the walk's first row size: walked again with room."""
+    rng = np.random.default_rng(2)
+    n = 700
+    ch, seg_len, pkt_seg = chains(rng, arena, n, max_seg=300, max_len=40)
+    with registered(arena, ch.mbufs):
+        u.set_tuning("walk_device", 1)
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 30, 3))
+    assert nw == 1
+    assert np.array_equal(got, ora.skip_batch(ch.heads, 1 << 30, 3))
+
+
+def test_device_walk_falls_back_outside_regions(ora, arena):
+    """A chain whose mbufs, or one of whose data pointers, lie outside the
+    registered regions goes to the host walk, with the same results."""
+    rng = np.random.default_rng(3)
+    n = 2000
+    ch, _, _ = chains(rng, arena, n)
+    want = ora.skip_batch(ch.heads, 1 << 20, 0)
+    with registered(arena):  # mbufs not registered
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 20, 0))
+    assert nw == 0 and np.array_equal(got, want)
+    # one mbuf mid-chain points into an unregistered buffer
+    other = rand_arena(1 << 16, 9)
+    long_pk = int(np.flatnonzero(np.diff(ch.pkt_seg) >= 3)[0])
+    mid = int(ch.pkt_seg[long_pk]) + 1
+    ch.mbufs["m_data"][mid] = other.ctypes.data
+    ch.mbufs["m_len"][mid] = 64
+    want = ora.skip_batch(ch.heads, 1 << 20, 0)
+    with registered(arena, ch.mbufs):
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 20, 0))
+    assert nw == 0 and np.array_equal(got, want)
+    with registered(arena, ch.mbufs, other):  # now it is registered too
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 20, 0))
+    assert nw == 1 and np.array_equal(got, want)
+
+
+def test_device_walk_pseudo_header(ora, arena):
+    """in_cksum_pseudo_header_batch: off0 inside the first mbuf walks on the
+    GPU; an off0 past the first mbuf (where the reference's sum differs from
+    the skip form) takes the host walk."""
+    rng = np.random.default_rng(4)
+    n = 3000
+    ch, seg_len, pkt_seg = chains(rng, arena, n, zero_frac=0.0)
+    first = seg_len[pkt_seg[:-1]]
+    cs = np.concatenate([[0], np.cumsum(seg_len)])
+    tot = cs[pkt_seg[1:]] - cs[pkt_seg[:-1]]
+    off0 = np.minimum(first, rng.integers(0, 41, n))
+    plen = np.maximum(0, tot - off0 - rng.integers(0, 20, n))
+    src, dst = (rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) for _ in range(2))
+    proto = rng.choice(np.array([6, 17], np.uint8), n)
+    want = ora.pseudo_header_batch(ch.heads, plen, off0, src, dst, proto)
+    with registered(arena, ch.mbufs):
+        got, nw = walks(lambda: u.in_cksum_pseudo_header_batch(ch.heads, plen, off0, src, dst, proto))
+        assert nw == 1 and np.array_equal(got, want)
+        off0b = off0.copy()
+        off0b[5] = first[5] + 3  # outside the reference's contract: host walk
+        plenb = np.maximum(0, plen - 3)
+        wantb = ora.pseudo_header_batch(ch.heads, plenb, off0b, src, dst, proto)
+        got, nw = walks(lambda: u.in_cksum_pseudo_header_batch(ch.heads, plenb, off0b, src, dst,
+                                                                proto))
+    assert nw == 0 and np.array_equal(got, wantb)
+
+
+def test_device_walk_knob_off(ora, arena):
+    rng = np.random.default_rng(5)
+    ch, _, _ = chains(rng, arena, 500)
+    try:
+        u.set_tuning("walk_device", 0)
+        with registered(arena, ch.mbufs):
+            got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 20, 0))
+    finally:
+        u.set_tuning("walk_device", 1)
+    assert nw == 0 and np.array_equal(got, ora.skip_batch(ch.heads, 1 << 20, 0))
+
+
+def test_device_walk_hooks(ora, torch_dev):
+    """The RX / TX hooks (headers parsed on the host, payload chains walked on
+    the GPU), mbufs and frames registered (in6_cksum_batch: tests/test_in6.py)."""
+    from libuinet_amd.frames import FrameBatch, pkthdr_fields
+
+    a = FrameBatch(3000, seed=11, ipv6=0.3)
+    b = FrameBatch(3000, seed=11, ipv6=0.3)
+    with registered(a.arena, a.tx.mbufs):
+        st, nw = walks(lambda: u.tx_offload(a.tx.heads))
+    assert nw == 1
+    assert np.array_equal(st, ora.tx_offload(b.tx.heads))
+    assert np.array_equal(a.arena, b.arena)
+    for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
+        assert np.array_equal(x, y)
+    rx_a, arena_a, _ = a.rx(seed=3, corrupt=0.05)
+    rx_b, _, _ = b.rx(seed=3, corrupt=0.05)
+    with registered(arena_a, rx_a.mbufs):
+        st, nw = walks(lambda: u.rx_offload(rx_a.heads))
+    assert nw == 1
+    assert np.array_equal(st, ora.rx_offload(rx_b.heads))
+    for x, y in zip(pkthdr_fields(rx_a), pkthdr_fields(rx_b)):
+        assert np.array_equal(x, y)
+
+
+def test_host_cpu_counters(arena):
+    """uinet_cksum_host_cpu counts calls, packets, wall and CPU time on the
+    calling thread, and resets."""
+    rng = np.random.default_rng(6)
+    ch, _, _ = chains(rng, arena, 5000)
+    u.host_cpu(reset=True)
+    u.in_cksum_skip_batch(ch.heads, 1 << 20, 0)
+    u.in_cksum_skip_batch(ch.heads, 1 << 20, 0)
+    st = u.host_cpu(reset=True)
+    assert st["calls"] == 2 and st["packets"] == 10000
+    assert st["wall_ns"] > 0 and st["caller_cpu_ns"] > 0
+    assert st["cpu_ns"] == st["caller_cpu_ns"] + st["helper_cpu_ns"]
+    assert u.host_cpu()["calls"] == 0

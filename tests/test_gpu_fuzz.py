@@ -125,7 +125,8 @@ def test_fuzz_device_entry_points(ora):
             u.set_tuning(k, v)
 
 
-HOST_DEFAULTS = {"host_threads": min(16, os.cpu_count() or 1), "walk_prefetch": 1, "host_pin": 0}
+HOST_DEFAULTS = {"host_threads": min(16, os.cpu_count() or 1), "walk_prefetch": 1, "host_pin": 0,
+                 "walk_device": 1}
 
 
 def _host_trial(ora, arena, t):
@@ -135,6 +136,7 @@ def _host_trial(ora, arena, t):
     u.set_tuning("host_threads", int(rng.choice([1, 2, 5, 16])))
     u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
     u.set_tuning("host_pin", int(rng.integers(0, 2)))
+    u.set_tuning("walk_device", int(rng.integers(0, 2)))
     n = int(rng.choice([1, 7, 64, int(rng.integers(1, 2500))]))
     nseg = rng.integers(1, int(rng.choice([2, 6, 30])) + 1, n)  # a chain is >= 1 mbuf
     pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
@@ -147,8 +149,12 @@ def _host_trial(ora, arena, t):
     cs = np.concatenate([[0], np.cumsum(seg_len)])
     tot = cs[pkt_seg[1:]] - cs[pkt_seg[:-1]]
     zero_copy = rng.random() < 0.5
+    # with the mbufs registered too, the GPU walks the chains (cksum_walk.hip)
+    walk_mbufs = zero_copy and rng.random() < 0.5
     if zero_copy:
         u.register_host(arena)
+    if walk_mbufs:
+        u.register_host(ch.mbufs)
     try:
         if rng.random() < 0.7:
             length = np.maximum(0, tot + rng.integers(-30, 31, n)).astype(np.int64)
@@ -167,8 +173,11 @@ def _host_trial(ora, arena, t):
     finally:
         if zero_copy:
             u.unregister_host(arena)
+        if walk_mbufs:
+            u.unregister_host(ch.mbufs)
     bad = np.flatnonzero(got != want)
     assert bad.size == 0, (f"host trial {t}: {what} n={n} zero_copy={zero_copy} "
+                           f"mbufs registered={walk_mbufs} "
                            f"first mismatches {bad[:5].tolist()}")
     return n
 
@@ -206,6 +215,7 @@ def test_fuzz_offload_hooks(ora):
             rng = np.random.default_rng(50000 + t)
             u.set_tuning("host_threads", int(rng.choice([1, 3, 16])))
             u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
+            u.set_tuning("walk_device", int(rng.integers(0, 2)))
             n = int(rng.choice([1, 2, int(rng.integers(1, 1500))]))
             l2 = bool(rng.integers(0, 2))
             l2len = -1 if l2 else 0
@@ -214,15 +224,20 @@ def test_fuzz_offload_hooks(ora):
             a = FrameBatch(n, seed=seed, l2=l2, ipv6=ipv6)
             b = FrameBatch(n, seed=seed, l2=l2, ipv6=ipv6)
             zc = bool(rng.integers(0, 2))
+            mb = zc and bool(rng.integers(0, 2))  # mbufs registered: the GPU walks
             if zc:
                 u.register_host(a.arena)
+            if mb:
+                u.register_host(a.tx.mbufs)
             try:
                 st_g = u.tx_offload(a.tx.heads, l2len)
             finally:
                 if zc:
                     u.unregister_host(a.arena)
+                if mb:
+                    u.unregister_host(a.tx.mbufs)
             st_o = ora.tx_offload(b.tx.heads, l2len)
-            ctx = f"offload trial {t}: n={n} l2={l2} ipv6={ipv6} zero_copy={zc}"
+            ctx = f"offload trial {t}: n={n} l2={l2} ipv6={ipv6} zero_copy={zc} mbufs={mb}"
             assert np.array_equal(st_g, st_o), ctx + " (TX status)"
             assert np.array_equal(a.arena, b.arena), ctx + " (TX bytes)"
             for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
@@ -233,11 +248,15 @@ def test_fuzz_offload_hooks(ora):
             rx_b, _, _ = b.rx(seed=rs, corrupt=corrupt)
             if zc:
                 u.register_host(arena_a)
+            if mb:
+                u.register_host(rx_a.mbufs)
             try:
                 st_g = u.rx_offload(rx_a.heads, l2len)
             finally:
                 if zc:
                     u.unregister_host(arena_a)
+                if mb:
+                    u.unregister_host(rx_a.mbufs)
             st_o = ora.rx_offload(rx_b.heads, l2len)
             assert np.array_equal(st_g, st_o), ctx + f" corrupt={corrupt} (RX status)"
             for x, y in zip(pkthdr_fields(rx_a), pkthdr_fields(rx_b)):

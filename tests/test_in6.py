@@ -207,5 +207,13 @@ def test_in6_gpu(torch_dev, v6, ora):
     u.register_host(ch.arena)
     try:
         np.testing.assert_array_equal(u.in6_cksum_batch(ch.heads, nxt, off, ln), want)
+        # the mbufs registered too: the GPU walks the chains (csrc/cksum_walk.hip)
+        u.register_host(ch.mbufs)
+        try:
+            w0 = u.host_cpu()["device_walks"]
+            np.testing.assert_array_equal(u.in6_cksum_batch(ch.heads, nxt, off, ln), want)
+            assert u.host_cpu()["device_walks"] == w0 + 1
+        finally:
+            u.unregister_host(ch.mbufs)
     finally:
         u.unregister_host(ch.arena)
