@@ -27,6 +27,8 @@
 #include <string.h>
 
 #include <cxxabi.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -192,7 +194,7 @@ struct Ctx {
   uint16_t* h_out = nullptr;  // pinned results
   uint16_t* d_out = nullptr;
   size_t out_cap = 0;
-  hipEvent_t done = nullptr;  // blocking-sync event: the host sleeps while the GPU works
+  hipEvent_t done = nullptr;  // recorded after a batch; ctx_wait sleeps until it completes
   uint32_t walk_k = 0;        // device walk: segment slots per packet last needed
 };
 
@@ -219,24 +221,51 @@ int ctx_current(Ctx** out) {
   }
   if (!c.done) {
     rc = record_hip(
-        hipEventCreateWithFlags(&c.done, hipEventBlockingSync | hipEventDisableTiming));
+        hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
     if (rc) return rc;
   }
   *out = &c;
   return UINET_CKSUM_OK;
 }
 
-// Waits for everything queued on the context's stream.  A blocking-sync event
-// lets the calling thread sleep instead of polling for the whole fold (the
-// lab build -DUINET_WAIT_STREAM_SYNC polls with hipStreamSynchronize, for the
+// Waits for everything queued on the context's stream without burning the
+// calling core.  hipEventSynchronize / hipStreamSynchronize poll the
+// completion signal on this thread for the whole wait, even with
+// hipEventBlockingSync (round 5, profiles/r05/r05a2/: a device-walked
+// config-3 batch cost 11.5 ms of CPU in an 11.6-ms call).  Here the thread
+// polls the event for the first kSpinUs (a small batch's whole fold: no
+// added latency), then sleeps between polls for 1/32 of the time waited so
+// far (10 us to 1 ms; at most ~3 % added to a long wait), with the timer slack
+// at 1 us meanwhile so a short sleep is not stretched to the default 50 us.
+// The lab build -DUINET_WAIT_SPIN waits in hipEventSynchronize instead (the
 // CPU-time A/B in DESIGN.md).
+constexpr long kSpinUs = 50;
 int ctx_wait(Ctx& c) {
-#ifdef UINET_WAIT_STREAM_SYNC
-  return record_hip(hipStreamSynchronize(c.stream));
-#else
   int rc = record_hip(hipEventRecord(c.done, c.stream));
   if (rc) return rc;
+#ifdef UINET_WAIT_SPIN
   return record_hip(hipEventSynchronize(c.done));
+#else
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = clk::now();
+  int slack = -1;  // the thread's timer slack, restored on return
+  for (;;) {
+    const hipError_t e = hipEventQuery(c.done);
+    if (e != hipErrorNotReady) {
+      if (slack >= 0) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+      return record_hip(e);
+    }
+    const long us = (long)std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t0)
+                        .count();
+    if (us < kSpinUs) continue;
+    if (slack < 0) {
+      slack = (int)prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+      prctl(PR_SET_TIMERSLACK, 1ul, 0, 0, 0);
+    }
+    const long nap = std::min(1000l, std::max(10l, us / 32));
+    const timespec ts{0, nap * 1000};
+    nanosleep(&ts, nullptr);
+  }
 #endif
 }
 
@@ -633,7 +662,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
 // (head, len, skip, seed: 20 B per packet) into pinned memory; the GPU walks
 // the chains (k_walk_mbufs) into a K-slot segment list in HBM and folds it with
 // the chain kernel, reading mbuf headers and packet bytes in place over PCIe.
-// The host thread sleeps on a blocking-sync event meanwhile.
+// The host thread sleeps in ctx_wait meanwhile.
 
 enum WalkKind { kWalkNone = 0, kWalkSkip = 1, kWalkPseudo = 2 };
 constexpr uint32_t kWalkKMax = 4096;  // longer chains take the host walk

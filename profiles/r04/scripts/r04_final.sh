@@ -4,5 +4,5 @@
 # driver's sequence (every GPU test, smoke, the driver's bench command and
 # its trace) reading those entries.
 set -u
-TAG=${TAG:-r04s4} HBM=1 bash tools/r04_spanset.sh || exit 1
-TAG=${VTAG:-r04v3} bash tools/r04_verify.sh || exit 1
+TAG=${TAG:-r04s4} HBM=1 bash profiles/r04/scripts/r04_spanset.sh || exit 1
+TAG=${VTAG:-r04v3} bash profiles/r04/scripts/r04_verify.sh || exit 1

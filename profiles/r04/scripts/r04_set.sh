@@ -3,7 +3,7 @@
 # kernel trace and FETCH_SIZE pass (tools/prof_all.sh, folded into
 # profiles/pmc_traffic.json with the kernel's source hash), the chain
 # kernel's instruction counters, and the box's pure-read ceiling.
-# Usage: TAG=r04x CONFIGS="3 3+packed 3tx" bash tools/r04_set.sh
+# Usage: TAG=r04x CONFIGS="3 3+packed 3tx" bash profiles/r04/scripts/r04_set.sh
 set -u
 TAG=${TAG:-r04s}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null

@@ -7,7 +7,7 @@ set -u
 TAG=${TAG:-r04tl}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 LIB=libuinet_amd/libuinet_cksum.so
-TESTS="tests/test_chains32.py tests/test_chains_dense.py tests/test_variants.py" CONFIGS="3 3tx 5tso" TAG=$TAG bash tools/r04_c5.sh || exit 1
+TESTS="tests/test_chains32.py tests/test_chains_dense.py tests/test_variants.py" CONFIGS="3 3tx 5tso" TAG=$TAG bash profiles/r04/scripts/r04_c5.sh || exit 1
 cp $LIB tools/ab_so/keep.so; cp tools/ab_so/new.so $LIB
 for c in 3 3tx; do
   timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_c${c}_new" -o run --output-format csv -- python3 bench.py --config $c --steps 10 --warmup 2 --cpu-baseline off > "$OUT/pmc_c${c}_new.log" 2>&1 || { cp tools/ab_so/keep.so $LIB; exit 1; }

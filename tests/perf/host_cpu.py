@@ -94,10 +94,15 @@ class Regs:
             u.unregister_host(b)
 
 
+PATHS = ("staged", "zero_copy", "dev_walk")
+
+
 def run_paths(name, n, nbytes, fn, bytes_bufs, mbuf_bufs, threads, reps, check, res):
     """Every engine path x host_threads for one workload; check(out) -> bool."""
     paths = (("staged", []), ("zero_copy", bytes_bufs), ("dev_walk", bytes_bufs + mbuf_bufs))
     for path, bufs in paths:
+        if path not in PATHS:
+            continue
         for t in threads:
             u.set_tuning("host_threads", t)
             with Regs(bufs):
@@ -116,7 +121,10 @@ def main():
     ap.add_argument("--threads", default="1,16")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--c2-packets", type=int, default=1 << 20)
+    ap.add_argument("--paths", default=",".join(PATHS))
     a = ap.parse_args()
+    global PATHS
+    PATHS = tuple(a.paths.split(","))
     threads = [int(x) for x in a.threads.split(",")]
     work = a.work.split(",")
     R = oracle.Reference() if oracle.have_reference() else None
@@ -165,6 +173,9 @@ def main():
 
         run_paths("tx_hook", nf, nbytes, tx, [fb.arena], [fb.tx.mbufs], threads, a.reps,
                   lambda o: np.array_equal(o, st_o), res)
+        # the repeated TX runs re-summed fields that already held final sums:
+        # back to the state after one TX pass (the oracle's) before RX
+        fb.arena[:] = ref_fb.arena
         rx, arena_rx, _ = fb.rx(seed=7, corrupt=0.05)
         rx_o, _, _ = ref_fb.rx(seed=7, corrupt=0.05)
         want_rx = O.rx_offload(rx_o.heads)

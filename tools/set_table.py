@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Markdown table of a measurement set (tools/r04_set.sh / prof_all.sh):
+"""Markdown table of a measurement set (profiles/r04/scripts/r04_set.sh / prof_all.sh):
 one row per bench_<tag>.log, with its trace and FETCH_SIZE summaries.
 
 Usage: set_table.py profiles/r04/r04s1 [profiles/r04/r04s2 ...]"""
