@@ -195,6 +195,8 @@ struct Ctx {
   uint16_t* d_out = nullptr;
   size_t out_cap = 0;
   hipEvent_t done = nullptr;  // recorded after a batch; ctx_wait sleeps until it completes
+  hipStream_t side = nullptr;  // device walk: the second stream of the walk/fold pipeline
+  hipEvent_t fork = nullptr, join = nullptr;
   uint32_t walk_k = 0;        // device walk: segment slots per packet last needed
 };
 
@@ -666,6 +668,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
 
 enum WalkKind { kWalkNone = 0, kWalkSkip = 1, kWalkPseudo = 2 };
 constexpr uint32_t kWalkKMax = 4096;  // longer chains take the host walk
+constexpr int kWalkGroupMin = 16384;  // packets per walk/fold pipeline group, at least
 
 // job(i) -> Job (the in_cksum_skip form; len and skip as the caller gave
 // them).  Returns kFallback (nothing delivered) when the batch must take the
@@ -731,35 +734,62 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
   if (rc) return rc;
   const uint8_t* dj = static_cast<const uint8_t*>(dh);
   volatile uint32_t* st = reinterpret_cast<volatile uint32_t*>(h + h_st);
+  // Groups of consecutive packets alternate between the context's stream and
+  // a side stream, each group's walk then its fold: group g + 1's walk (a
+  // chase of dependent PCIe reads) runs while group g's fold streams its
+  // bytes.  The side stream starts after the status reset and the main stream
+  // copies the status back after the side stream's last fold.
+#ifndef UINET_WALK_GROUPS  // lab A/B: -DUINET_WALK_GROUPS=1 walks the batch in one group
+#define UINET_WALK_GROUPS 8
+#endif
+  const int groups = n >= 2 * kWalkGroupMin ? std::min(UINET_WALK_GROUPS, n / kWalkGroupMin) : 1;
+  if (groups > 1 && !c.side) {
+    rc = record_hip(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    if (!rc) rc = record_hip(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+    if (!rc) rc = record_hip(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
+    if (rc) return rc;
+  }
   for (int attempt = 0; attempt < 2; attempt++) {
     rc = ctx_reserve(c, h_end, N, dev_layout(K, &d_sl, &d_ps, &d_ln, &d_sk, &d_sd, &d_st));
     if (rc) return rc;
     uint8_t* d = c.d_buf;
     rc = record_hip(hipMemsetAsync(d + d_st, 0, 8, c.stream));
-    if (rc) return rc;
-    rc = launch_walk_mbufs(reinterpret_cast<const uint64_t*>(dj),
-                           reinterpret_cast<const int32_t*>(dj + h_len),
-                           reinterpret_cast<const int32_t*>(dj + h_skip),
-                           seeded ? reinterpret_cast<const uint32_t*>(dj + h_seed) : nullptr,
-                           reinterpret_cast<const WalkRegionHost*>(dj + h_reg), (int)nreg,
-                           (uint32_t)n, K, lo_addr, kind == kWalkPseudo,
-                           reinterpret_cast<uint64_t*>(d), reinterpret_cast<uint32_t*>(d + d_sl),
-                           reinterpret_cast<uint32_t*>(d + d_ps),
-                           reinterpret_cast<uint32_t*>(d + d_ln),
-                           reinterpret_cast<uint32_t*>(d + d_sk),
-                           reinterpret_cast<uint32_t*>(d + d_sd),
-                           reinterpret_cast<uint32_t*>(d + d_st), c.stream);
-    if (!rc)
-      rc = launch_chains(reinterpret_cast<const void*>(lo_addr),
-                         reinterpret_cast<const uint64_t*>(d),
-                         reinterpret_cast<const uint32_t*>(d + d_sl),
-                         reinterpret_cast<const uint32_t*>(d + d_ps),
-                         reinterpret_cast<const uint32_t*>(d + d_ln),
-                         reinterpret_cast<const uint32_t*>(d + d_sk),
-                         seeded ? reinterpret_cast<const uint32_t*>(d + d_sd) : nullptr,
-                         static_cast<uint16_t*>(dout), (uint32_t)n, flags, 0, c.stream);
+    if (!rc && groups > 1) rc = record_hip(hipEventRecord(c.fork, c.stream));
+    if (!rc && groups > 1) rc = record_hip(hipStreamWaitEvent(c.side, c.fork, 0));
+    for (int g = 0; g < groups && !rc; g++) {
+      const size_t i0 = N * (size_t)g / (size_t)groups, i1 = N * (size_t)(g + 1) / (size_t)groups;
+      const uint32_t ng = (uint32_t)(i1 - i0);
+      hipStream_t sg = (g & 1) ? c.side : c.stream;
+      rc = launch_walk_mbufs(reinterpret_cast<const uint64_t*>(dj) + i0,
+                             reinterpret_cast<const int32_t*>(dj + h_len) + i0,
+                             reinterpret_cast<const int32_t*>(dj + h_skip) + i0,
+                             seeded ? reinterpret_cast<const uint32_t*>(dj + h_seed) + i0 : nullptr,
+                             reinterpret_cast<const WalkRegionHost*>(dj + h_reg), (int)nreg, ng, K,
+                             (uint32_t)(i0 * K), lo_addr, kind == kWalkPseudo,
+                             reinterpret_cast<uint64_t*>(d) + i0 * K,
+                             reinterpret_cast<uint32_t*>(d + d_sl) + i0 * K,
+                             reinterpret_cast<uint32_t*>(d + d_ps) + i0,
+                             reinterpret_cast<uint32_t*>(d + d_ln) + i0,
+                             reinterpret_cast<uint32_t*>(d + d_sk) + i0,
+                             reinterpret_cast<uint32_t*>(d + d_sd) + i0,
+                             reinterpret_cast<uint32_t*>(d + d_st), sg);
+      // the group's rows are indexed from the list's row 0 (pkt_seg holds
+      // global row numbers)
+      if (!rc)
+        rc = launch_chains(reinterpret_cast<const void*>(lo_addr),
+                           reinterpret_cast<const uint64_t*>(d),
+                           reinterpret_cast<const uint32_t*>(d + d_sl),
+                           reinterpret_cast<const uint32_t*>(d + d_ps) + i0,
+                           reinterpret_cast<const uint32_t*>(d + d_ln) + i0,
+                           reinterpret_cast<const uint32_t*>(d + d_sk) + i0,
+                           seeded ? reinterpret_cast<const uint32_t*>(d + d_sd) + i0 : nullptr,
+                           static_cast<uint16_t*>(dout) + i0, ng, flags, 0, sg);
+    }
+    if (!rc && groups > 1) rc = record_hip(hipEventRecord(c.join, c.side));
+    if (!rc && groups > 1) rc = record_hip(hipStreamWaitEvent(c.stream, c.join, 0));
     if (!rc)
       rc = record_hip(hipMemcpyAsync(h + h_st, d + d_st, 8, hipMemcpyDeviceToHost, c.stream));
+    if (rc && groups > 1) (void)hipStreamSynchronize(c.side);  // nothing left running
     const int wrc = ctx_wait(c);
     if (rc) return rc;
     if (wrc) return wrc;

@@ -99,13 +99,14 @@ constexpr uint32_t kWalkFallback = 1;  // status[0]: a job the host walk must ta
 constexpr uint32_t kWalkUnmapped = 2;  // status[0]: a pointer outside the regions
 // Packet i's chain (heads[i], len[i], skip[i], seed[i]; seed may be NULL) into
 // row i of a K-slot segment list in HBM (seg_off relative to lo_dev; pkt_seg
-// = i * K), plus u32 len / skip / seed arrays for launch_chains.  status (2 u32
+// [i] = seg_base + i * K, the row's index in a list of which seg_off / seg_len
+// are row 0), plus u32 len / skip / seed arrays for launch_chains.  status (2 u32
 // in device memory, zeroed by the caller): [0] kWalk* bits, [1] the longest
 // chain when one exceeds K.  `pseudo`: the in_cksum_pseudo_header form (skip
 // = off0 must lie within the first mbuf).
 int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* skip,
                       const uint32_t* seed, const WalkRegionHost* regions, int nreg, uint32_t n,
-                      uint32_t K, uint64_t lo_dev, bool pseudo, uint64_t* seg_off,
+                      uint32_t K, uint32_t seg_base, uint64_t lo_dev, bool pseudo, uint64_t* seg_off,
                       uint32_t* seg_len, uint32_t* pkt_seg, uint32_t* len_out, uint32_t* skip_out,
                       uint32_t* seed_out, uint32_t* status, hipStream_t stream);
 

@@ -4,8 +4,8 @@
 // netmap rings of uinet_if_netmap_host.c:153).
 //
 // The host hands over only the batch's jobs -- head mbuf pointer, len, skip,
-// seed per packet -- and the small table of registered regions.  One lane
-// per packet chases m_next / m_data / m_len (struct m_hdr offsets 0 / 16 /
+// seed per packet -- and the small table of registered regions.  A pair of
+// lanes per packet chases m_next / m_data / m_len (struct m_hdr offsets 0 / 16 /
 // 24, /root/reference/sys/sys/mbuf.h:90-98) over PCIe through the regions'
 // device aliases, exactly as far as in_cksum_skip reads the chain
 // (/root/reference/sys/amd64/amd64/in_cksum.c:203-229: until `len` bytes
@@ -33,21 +33,35 @@ namespace uinet {
 namespace {
 
 using WalkRegion = WalkRegionHost;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 GlobalU32x4;
 
+// The partner lane's value (lanes 2k and 2k + 1 swap): DPP quad_perm [1,0,3,2].
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+
+// Two lanes per packet.  The walk's rate is the number of PCIe reads in
+// flight over their latency, so what a hop costs is its requests: lanes 2k
+// and 2k + 1 load the two 16-B halves of the header's first 32 bytes in ONE
+// instruction, which the coalescer issues as one request for the line (one
+// lane loading both halves issues two), then swap halves over DPP.  Both
+// lanes of a pair follow the same chain, so their control flow is identical.
 __global__ __launch_bounds__(256) void k_walk_mbufs(
     const uint64_t* __restrict__ heads, const int32_t* __restrict__ jlen,
     const int32_t* __restrict__ jskip, const uint32_t* __restrict__ jseed,
-    const WalkRegion* __restrict__ regions, int nreg, uint32_t n, uint32_t K, uint64_t lo_dev,
-    int pseudo, uint64_t* __restrict__ seg_off, uint32_t* __restrict__ seg_len,
+    const WalkRegion* __restrict__ regions, int nreg, uint32_t n, uint32_t K, uint32_t seg_base,
+    uint64_t lo_dev, int pseudo, uint64_t* __restrict__ seg_off, uint32_t* __restrict__ seg_len,
     uint32_t* __restrict__ pkt_seg, uint32_t* __restrict__ len_out,
     uint32_t* __restrict__ skip_out, uint32_t* __restrict__ seed_out,
     uint32_t* __restrict__ status) {
   __shared__ WalkRegion R[kWalkRegionsMax];
   for (int k = (int)threadIdx.x; k < nreg; k += (int)blockDim.x) R[k] = regions[k];
   __syncthreads();
-  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t half = threadIdx.x & 1;  // which 16 B of the header this lane loads
+  const uint32_t stride = (gridDim.x * blockDim.x) >> 1;
   uint32_t any_bad = 0, longest = 0;  // this lane's, over its packets
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1; i < n; i += stride) {
     const uint64_t head = heads[i];
     const int32_t L = jlen[i], S = jskip[i];
     const uint32_t lim = L < 0 ? 0u : (uint32_t)L;  // len < 0: nothing is summed
@@ -61,10 +75,14 @@ __global__ __launch_bounds__(256) void k_walk_mbufs(
         bad = kWalkUnmapped;
         break;
       }
-      const uint64_t* h = reinterpret_cast<const uint64_t*>(dm);
-      const uint64_t next = h[0];
-      const uint64_t data = h[2];
-      const int32_t ml = reinterpret_cast<const int32_t*>(dm)[6];
+      // lane 0 of the pair: m_next, m_nextpkt; lane 1: m_data, m_len, m_flags
+      const u32x4 v = reinterpret_cast<const GlobalU32x4*>(dm)[half];
+      const uint32_t w0 = pair_swap(v.x), w1 = pair_swap(v.y), w2 = pair_swap(v.z);
+      const uint64_t next = half ? ((uint64_t)w0 | (uint64_t)w1 << 32)
+                                 : ((uint64_t)v.x | (uint64_t)v.y << 32);
+      const uint64_t data = half ? ((uint64_t)v.x | (uint64_t)v.y << 32)
+                                 : ((uint64_t)w0 | (uint64_t)w1 << 32);
+      const int32_t ml = (int32_t)(half ? v.z : w2);
       if (ml < 0 || (pseudo && cnt == 0 && ml < S)) {
         bad = kWalkFallback;
         break;
@@ -78,25 +96,28 @@ __global__ __launch_bounds__(256) void k_walk_mbufs(
         }
         off = dd - lo_dev;
       }
-      if (cnt < K) {
-        seg_off[row + cnt] = off;
-        seg_len[row + cnt] = (uint32_t)ml;
+      if (cnt < K) {  // one store each
+        if (half) seg_len[row + cnt] = (uint32_t)ml;
+        else seg_off[row + cnt] = off;
       }
       cnt++;
       cum += (uint64_t)ml;
       m = next;
     }
     for (uint32_t k = cnt; k < K; k++) {
-      seg_off[row + k] = 0;
-      seg_len[row + k] = 0;
+      if (half) seg_len[row + k] = 0;
+      else seg_off[row + k] = 0;
     }
     any_bad |= bad;
     longest = max(longest, cnt);
-    pkt_seg[i] = i * K;
-    if (i == n - 1) pkt_seg[n] = n * K;
-    len_out[i] = lim;
-    skip_out[i] = (uint32_t)S;
-    seed_out[i] = jseed ? jseed[i] : 0u;
+    if (!half) {
+      pkt_seg[i] = seg_base + i * K;
+      if (i == n - 1) pkt_seg[n] = seg_base + n * K;
+      len_out[i] = lim;
+      skip_out[i] = (uint32_t)S;
+    } else {
+      seed_out[i] = jseed ? jseed[i] : 0u;
+    }
   }
   // one atomic per wave: the status bits and the longest chain (the host
   // sizes the next batch's rows by it)
@@ -114,19 +135,19 @@ __global__ __launch_bounds__(256) void k_walk_mbufs(
 
 int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* skip,
                       const uint32_t* seed, const WalkRegionHost* regions, int nreg, uint32_t n,
-                      uint32_t K, uint64_t lo_dev, bool pseudo, uint64_t* seg_off,
+                      uint32_t K, uint32_t seg_base, uint64_t lo_dev, bool pseudo, uint64_t* seg_off,
                       uint32_t* seg_len, uint32_t* pkt_seg, uint32_t* len_out, uint32_t* skip_out,
                       uint32_t* seed_out, uint32_t* status, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
-  if (nreg < 1 || nreg > kWalkRegionsMax || K == 0 || (uint64_t)n * K > 0xffffffffull)
+  if (nreg < 1 || nreg > kWalkRegionsMax || K == 0 ||
+      (uint64_t)seg_base + (uint64_t)n * K > 0xffffffffull)
     return UINET_CKSUM_EINVAL;
-  // one lane per packet, every chain in flight at once: the walk is a chase of
-  // dependent PCIe reads, so its time is hops x latency when the grid covers
-  // the batch (256 CUs x 2048 lanes)
-  const uint64_t blocks64 = ((uint64_t)n + 255) / 256;
+  // two lanes per packet, every chain in flight at once (up to 1 M packets
+  // per pass of the grid)
+  const uint64_t blocks64 = (2 * (uint64_t)n + 255) / 256;
   const int blocks = (int)(blocks64 < 8192 ? blocks64 : 8192);
   UINET_LAUNCH(k_walk_mbufs, dim3(blocks), dim3(256), 0, stream, heads, len, skip, seed,
-               regions, nreg, n, K, lo_dev, pseudo ? 1 : 0,
+               regions, nreg, n, K, seg_base, lo_dev, pseudo ? 1 : 0,
                seg_off, seg_len, pkt_seg, len_out, skip_out, seed_out, status);
   return check_launch();
 }

@@ -121,7 +121,7 @@ def main():
     ap.add_argument("--threads", default="1,16")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--c2-packets", type=int, default=1 << 20)
-    ap.add_argument("--paths", default=",".join(PATHS))
+    ap.add_argument("--paths", default="staged,zero_copy,dev_walk")
     a = ap.parse_args()
     global PATHS
     PATHS = tuple(a.paths.split(","))

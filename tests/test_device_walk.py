@@ -93,6 +93,39 @@ def test_device_walk_long_chains_grow_rows(ora, arena):
     assert np.array_equal(got, ora.skip_batch(ch.heads, 1 << 30, 3))
 
 
+def test_device_walk_pipelined_groups(ora, arena):
+    """A batch large enough for the walk/fold pipeline (groups of consecutive
+    packets alternating between two streams), with a row size that has to
+    grow on the way (a few long chains), and skip / len cutting the chains."""
+    rng = np.random.default_rng(7)
+    n = 100_003
+    ch, seg_len, pkt_seg = chains(rng, arena, n, max_seg=5, max_len=200)
+    cs = np.concatenate([[0], np.cumsum(seg_len)])
+    tot = cs[pkt_seg[1:]] - cs[pkt_seg[:-1]]
+    length = np.maximum(0, tot - rng.integers(0, 30, n))
+    skip = np.minimum(rng.integers(0, 41, n), length)
+    want = ora.skip_batch(ch.heads, length, skip)
+    with registered(arena, ch.mbufs):
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, length, skip))
+        assert nw == 1 and np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+        # chains of up to 60 mbufs near the end of the batch: the walk grows its rows
+        long = MbufChains(arena, *_long_tail(rng, arena, n))
+        with registered(long.mbufs):
+            want2 = ora.skip_batch(long.heads, 1 << 30, 0)
+            got2, nw2 = walks(lambda: u.in_cksum_skip_batch(long.heads, 1 << 30, 0))
+    assert nw2 == 1 and np.array_equal(got2, want2), np.flatnonzero(got2 != want2)[:8]
+
+
+def _long_tail(rng, arena, n):
+    nseg = rng.integers(1, 4, n)
+    nseg[-50:] = rng.integers(30, 61, 50)
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = rng.integers(0, 100, s)
+    seg_off = rng.integers(0, arena.size - 101, s).astype(np.int64)
+    return seg_off, seg_len, pkt_seg
+
+
 def test_device_walk_falls_back_outside_regions(ora, arena):
     """A chain whose mbufs, or one of whose data pointers, lie outside the
     registered regions goes to the host walk, with the same results."""
