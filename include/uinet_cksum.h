@@ -168,12 +168,16 @@ int uinet_cksum_device_ok(void);
  *                     (1) or floating (0, default)
  *   "multi_gather"    uinet_cksum_spans_multi: 0 = one RCCL gather when it
  *                     applies (default), 1 = always peer copies
+ *   "walk_device"     host-mbuf batches (2c, 2d) whose mbufs AND bytes lie in
+ *                     registered memory: 1 (default) the GPU walks the chains,
+ *                     the host only writes the jobs; 0 the host walks them
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU,
  * UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG, UINET_CKSUM_CHAINS_TILE,
  * UINET_CKSUM_XCD_REMAP, UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF,
- * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_PIPE, UINET_CKSUM_HOST_PIN and
- * UINET_CKSUM_MULTI_GATHER set the initial values. */
+ * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_PIPE, UINET_CKSUM_HOST_PIN,
+ * UINET_CKSUM_MULTI_GATHER and UINET_CKSUM_WALK_DEVICE set the initial
+ * values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
 /* ------------------------------------------------------------------------ */
@@ -266,8 +270,11 @@ int in6_cksum_batch(struct mbuf *const *m, const uint8_t *nxt,
  * (the netmap ring buffers, uinet_if_netmap_host.c:153; the UMA slabs behind
  * mbufs and clusters, uinet_vm_kern.c:48-51) once; a host-mbuf batch whose
  * bytes all lie in registered regions is then folded in place by the GPU over
- * PCIe -- the host only walks the chains, it copies no packet bytes.  Other
- * batches are staged through pinned memory as before.  Regions must not
+ * PCIe -- the host only walks the chains, it copies no packet bytes.  When the
+ * mbufs themselves lie in registered regions too, the GPU also walks the
+ * chains (m_next / m_data / m_len read over PCIe; knob "walk_device"): the host
+ * writes 20 bytes of job per packet and sleeps until the results are back.
+ * Other batches are staged through pinned memory as before.  Regions must not
  * overlap; memory that is already pinned (hipHostMalloc) is accepted as is.
  * Unregistering waits for the batches in flight that may read the region;
  * batches on different threads run concurrently. */

@@ -14,6 +14,8 @@ leaves a packet: packet ``i`` is the in-order list of mbufs
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 MSIZE = 256
@@ -49,10 +51,27 @@ assert MBUF_DTYPE.fields["csum_flags"][1] == 64 and MBUF_DTYPE.fields["csum_data
 assert MBUF_DTYPE.fields["m_pktdat"][1] == 88
 
 
+HUGE = 2 << 20
+
+
 def aligned_empty(nbytes: int, align: int = 4096, pad: int = 64) -> np.ndarray:
-    """A uint8 buffer whose element 0 is ``align``-aligned, with ``pad`` bytes of
-    readable slack before and after it (the reference reads whole aligned
-    words around a span, in_cksum.c:106-115,165-167)."""
+    """A zeroed uint8 buffer whose element 0 is ``align``-aligned, with ``pad``
+    bytes of readable slack before and after it (the reference reads whole
+    aligned words around a span, in_cksum.c:106-115,165-167).
+
+    With UINET_MBUF_HUGEPAGES=1 in the environment, buffers of 2 MiB and more
+    come from an anonymous mapping advised MADV_HUGEPAGE (transparent huge
+    pages, as a UMA arena mapped with huge pages would be: uinet_vm_kern.c
+    maps one region for every zone) -- the device walk's A/B of page size."""
+    if os.environ.get("UINET_MBUF_HUGEPAGES") == "1" and nbytes >= HUGE:
+        import mmap
+
+        size = (nbytes + 2 * pad + 2 * HUGE + HUGE - 1) // HUGE * HUGE
+        m = mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+        m.madvise(mmap.MADV_HUGEPAGE)
+        raw = np.frombuffer(m, dtype=np.uint8)
+        start = (-(raw.ctypes.data + pad)) % HUGE + pad  # 2 MiB aligned
+        return raw[start : start + nbytes]
     raw = np.zeros(nbytes + align + 2 * pad, dtype=np.uint8)
     start = (-(raw.ctypes.data + pad)) % align + pad
     return raw[start : start + nbytes]  # the view keeps `raw` alive

@@ -244,6 +244,14 @@ def main():
         res["echo/reference/1t"] = per_k(e, ne, nbytes)
         print(json.dumps({"echo/reference/1t": e}), flush=True)
     u.set_tuning("host_threads", min(16, os.cpu_count() or 1))
+    try:  # how much of the process is on transparent huge pages (UINET_MBUF_HUGEPAGES)
+        with open("/proc/self/smaps_rollup") as f:
+            res["anon_huge_kb"] = int(next(ln for ln in f if ln.startswith("AnonHugePages")).split()[1])
+        with open("/sys/kernel/mm/transparent_hugepage/enabled") as f:
+            res["thp_mode"] = f.read().strip()
+    except (OSError, StopIteration, ValueError):
+        pass
+    res["hugepages_env"] = os.environ.get("UINET_MBUF_HUGEPAGES", "")
     print(json.dumps(res), flush=True)
 
 

@@ -173,7 +173,8 @@ def test_set_tuning_validation():
     ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_pass", 4), ("chains_long", 0),
           ("chains_long", 16), ("chains_tile", 8), ("xcd_remap", 0), ("host_threads", 64),
           ("walk_prefetch", 0), ("spans_geo", 0), ("spans_geo", 32 * 16 + 3), ("spans_geo", 64 * 16 + 9),
-          ("host_pin", 1), ("multi_gather", 1), ("spans_pipe", 0), ("spans_pipe", 1)]
+          ("host_pin", 1), ("multi_gather", 1), ("spans_pipe", 0), ("spans_pipe", 1),
+          ("walk_device", 0), ("walk_device", 1)]
     # chains_variant, spans_lut, spans_contig and spans_pipe 2 (k_spans_pp)
     # were removed in round 3; spans_sdesc, host_group and walk_prefetch 2 in
     # round 4
@@ -182,7 +183,8 @@ def test_set_tuning_validation():
            ("spans_geo", 16 * 16 + 6), ("spans_geo", 5), ("spans_sdesc", 0), ("host_group", 1),
            ("chains_sweep", 2),
            ("host_pin", 2), ("multi_gather", 2), ("spans_pipe", 2), ("spans_pipe", 3), ("chains_variant", 0),
-           ("spans_lut", 1), ("spans_contig", 0), ("no_such_knob", 1)]
+           ("spans_lut", 1), ("spans_contig", 0), ("walk_device", 2), ("walk_device", -1),
+           ("no_such_knob", 1)]
     try:
         for k, v in ok:
             assert L.uinet_cksum_set_tuning(k.encode(), v) == 0, (k, v)
@@ -193,7 +195,8 @@ def test_set_tuning_validation():
         for k, v in [("blocks_per_cu", 0), ("chains_pass", 2), ("chains_long", 128),
                      ("chains_tile", 0), ("xcd_remap", 1),
                      ("host_threads", min(16, os.cpu_count() or 1)), ("walk_prefetch", 1),
-                     ("spans_geo", 0), ("host_pin", 0), ("multi_gather", 0), ("spans_pipe", 1)]:
+                     ("spans_geo", 0), ("host_pin", 0), ("multi_gather", 0), ("spans_pipe", 1),
+                     ("walk_device", 1)]:
             L.uinet_cksum_set_tuning(k.encode(), v)
 
 
