@@ -670,6 +670,104 @@ enum WalkKind { kWalkNone = 0, kWalkSkip = 1, kWalkPseudo = 2 };
 constexpr uint32_t kWalkKMax = 4096;  // longer chains take the host walk
 constexpr int kWalkGroupMin = 16384;  // packets per walk/fold pipeline group, at least
 
+// The HBM work area of a walk + fold of N jobs at K segment slots per job:
+// seg_off u64[N K] | seg_len u32[N K] | pkt_seg u32[N + 1] | len | skip | seed.
+struct WalkWork {
+  size_t sl, ps, ln, sk, sd, end;
+};
+WalkWork walk_work(size_t N, uint32_t K) {
+  const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+  WalkWork w;
+  w.sl = a16(8 * N * K);
+  w.ps = w.sl + a16(4 * N * K);
+  w.ln = w.ps + a16(4 * (N + 1));
+  w.sk = w.ln + a16(4 * N);
+  w.sd = w.sk + a16(4 * N);
+  w.end = w.sd + a16(4 * N);
+  return w;
+}
+
+// Enqueues the walk (k_walk_mbufs) and the fold (k_chains_pipe) of N jobs --
+// device-readable arrays jm / jl / js / jd (jd may be NULL) -- over the work
+// area at `wa` (HBM), results into `out`, status bits into `dstatus` (zeroed
+// by the caller, on c.stream, before this).  Groups of consecutive jobs
+// alternate between the context's stream and a side stream, each group's walk
+// then its fold: group g + 1's walk (a chase of dependent PCIe reads) runs
+// while group g's fold streams its bytes.  Everything ends on c.stream; on an
+// error nothing is left running.
+int launch_walk_fold(Ctx& c, const uint64_t* jm, const int32_t* jl, const int32_t* js,
+                     const uint32_t* jd, const WalkRegionHost* regs, int nreg, uint64_t lo,
+                     size_t N, uint32_t K, bool pseudo, uint8_t* wa, uint32_t* dstatus,
+                     uint16_t* out, uint32_t flags) {
+#ifndef UINET_WALK_GROUPS  // lab A/B: -DUINET_WALK_GROUPS=1 walks the batch in one group
+#define UINET_WALK_GROUPS 8
+#endif
+  const int n = (int)N;
+  const int groups = n >= 2 * kWalkGroupMin ? std::min(UINET_WALK_GROUPS, n / kWalkGroupMin) : 1;
+  int rc = UINET_CKSUM_OK;
+  if (groups > 1 && !c.side) {
+    rc = record_hip(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    if (!rc) rc = record_hip(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+    if (!rc) rc = record_hip(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
+    if (rc) return rc;
+  }
+  const WalkWork W = walk_work(N, K);
+  if (groups > 1) rc = record_hip(hipEventRecord(c.fork, c.stream));
+  if (!rc && groups > 1) rc = record_hip(hipStreamWaitEvent(c.side, c.fork, 0));
+  for (int g = 0; g < groups && !rc; g++) {
+    const size_t i0 = N * (size_t)g / (size_t)groups, i1 = N * (size_t)(g + 1) / (size_t)groups;
+    const uint32_t ng = (uint32_t)(i1 - i0);
+    hipStream_t sg = (g & 1) ? c.side : c.stream;
+    rc = launch_walk_mbufs(jm + i0, jl + i0, js + i0, jd ? jd + i0 : nullptr, regs, nreg, ng, K,
+                           (uint32_t)(i0 * K), lo, pseudo,
+                           reinterpret_cast<uint64_t*>(wa) + i0 * K,
+                           reinterpret_cast<uint32_t*>(wa + W.sl) + i0 * K,
+                           reinterpret_cast<uint32_t*>(wa + W.ps) + i0,
+                           reinterpret_cast<uint32_t*>(wa + W.ln) + i0,
+                           reinterpret_cast<uint32_t*>(wa + W.sk) + i0,
+                           reinterpret_cast<uint32_t*>(wa + W.sd) + i0, dstatus, sg);
+    // the group's rows are indexed from the list's row 0 (pkt_seg holds
+    // global row numbers)
+    if (!rc)
+      rc = launch_chains(reinterpret_cast<const void*>(lo), reinterpret_cast<const uint64_t*>(wa),
+                         reinterpret_cast<const uint32_t*>(wa + W.sl),
+                         reinterpret_cast<const uint32_t*>(wa + W.ps) + i0,
+                         reinterpret_cast<const uint32_t*>(wa + W.ln) + i0,
+                         reinterpret_cast<const uint32_t*>(wa + W.sk) + i0,
+                         jd ? reinterpret_cast<const uint32_t*>(wa + W.sd) + i0 : nullptr,
+                         out + i0, ng, flags, 0, sg);
+  }
+  if (!rc && groups > 1) rc = record_hip(hipEventRecord(c.join, c.side));
+  if (!rc && groups > 1) rc = record_hip(hipStreamWaitEvent(c.stream, c.join, 0));
+  if (rc && groups > 1) (void)hipStreamSynchronize(c.side);  // nothing left running
+  return rc;
+}
+
+// The region table in the form the device walk reads, and the lowest device
+// address of a registered byte (the chain kernel's base).  0 regions or more
+// than the walk takes: false.  Called with g_reg_mu held.
+bool walk_regions(WalkRegionHost* R, size_t cap, size_t* nreg, uint64_t* lo) {
+  const size_t n = g_regions.size();
+  if (n == 0 || n > (size_t)kWalkRegionsMax || n > cap) return false;
+  uint64_t l = ~0ull;
+  for (size_t k = 0; k < n; k++) {
+    const Region& r = g_regions[k];
+    R[k] = WalkRegionHost{r.base, r.end, (int64_t)r.delta};
+    l = std::min(l, (uint64_t)(r.base + r.delta));
+  }
+  *nreg = n;
+  *lo = l;
+  return true;
+}
+
+// Next row size from the longest chain seen (the next batch on this thread
+// starts from it).
+uint32_t walk_k_for(uint32_t longest) {
+  uint32_t k = 4;
+  while (k < longest) k *= 2;
+  return k;
+}
+
 // job(i) -> Job (the in_cksum_skip form; len and skip as the caller gave
 // them).  Returns kFallback (nothing delivered) when the batch must take the
 // host walk.  Called with g_reg_mu held (shared) and at least one region.
@@ -679,30 +777,17 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
                       unsigned* out32, bool trace) {
   using clk = std::chrono::steady_clock;
   const clk::time_point t0 = trace ? clk::now() : clk::time_point();
-  const size_t nreg = g_regions.size();
-  if (nreg == 0 || nreg > (size_t)kWalkRegionsMax) return kFallback;
-  uint64_t lo_addr = ~0ull;
-  for (const Region& r : g_regions) lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
+  const size_t nreg_all = g_regions.size();
+  if (nreg_all == 0 || nreg_all > (size_t)kWalkRegionsMax) return kFallback;
   uint32_t K = c.walk_k ? c.walk_k : 4;
   const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const size_t N = (size_t)n;
   // pinned: heads u64 | len i32 | skip i32 | seed u32 | regions | status u32[2]
   const size_t h_len = a16(8 * N), h_skip = h_len + a16(4 * N), h_seed = h_skip + a16(4 * N);
   const size_t h_reg = h_seed + (seeded ? a16(4 * N) : 0);
-  const size_t h_st = h_reg + a16(sizeof(WalkRegionHost) * nreg), h_end = h_st + 16;
-  // HBM: seg_off u64[n K] | seg_len u32[n K] | pkt_seg u32[n + 1] | len | skip | seed | status
-  const auto dev_layout = [&](uint32_t k, size_t* o_sl, size_t* o_ps, size_t* o_ln, size_t* o_sk,
-                              size_t* o_sd, size_t* o_st) {
-    *o_sl = a16(8 * N * k);
-    *o_ps = *o_sl + a16(4 * N * k);
-    *o_ln = *o_ps + a16(4 * (N + 1));
-    *o_sk = *o_ln + a16(4 * N);
-    *o_sd = *o_sk + a16(4 * N);
-    *o_st = *o_sd + a16(4 * N);
-    return *o_st + 16;
-  };
-  size_t d_sl, d_ps, d_ln, d_sk, d_sd, d_st;
-  int rc = ctx_reserve(c, h_end, N, dev_layout(K, &d_sl, &d_ps, &d_ln, &d_sk, &d_sd, &d_st));
+  const size_t h_st = h_reg + a16(sizeof(WalkRegionHost) * nreg_all), h_end = h_st + 16;
+  // HBM: status u32[4] | the walk's work area
+  int rc = ctx_reserve(c, h_end, N, 16 + walk_work(N, K).end);
   if (rc) return rc;
   uint8_t* h = c.h_buf;
   uint64_t* heads = reinterpret_cast<uint64_t*>(h);
@@ -722,9 +807,9 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
       if (seeded) jd[i] = J.seed;
     }
   }, tuning().host_pin != 0);
-  WalkRegionHost* R = reinterpret_cast<WalkRegionHost*>(h + h_reg);
-  for (size_t k = 0; k < nreg; k++)
-    R[k] = WalkRegionHost{g_regions[k].base, g_regions[k].end, (int64_t)g_regions[k].delta};
+  size_t nreg = 0;
+  uint64_t lo_addr = 0;
+  (void)walk_regions(reinterpret_cast<WalkRegionHost*>(h + h_reg), nreg_all, &nreg, &lo_addr);
   const clk::time_point t1 = trace ? clk::now() : clk::time_point();
   void* dh = nullptr;
   rc = record_hip(hipHostGetDevicePointer(&dh, c.h_buf, 0));
@@ -734,70 +819,28 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
   if (rc) return rc;
   const uint8_t* dj = static_cast<const uint8_t*>(dh);
   volatile uint32_t* st = reinterpret_cast<volatile uint32_t*>(h + h_st);
-  // Groups of consecutive packets alternate between the context's stream and
-  // a side stream, each group's walk then its fold: group g + 1's walk (a
-  // chase of dependent PCIe reads) runs while group g's fold streams its
-  // bytes.  The side stream starts after the status reset and the main stream
-  // copies the status back after the side stream's last fold.
-#ifndef UINET_WALK_GROUPS  // lab A/B: -DUINET_WALK_GROUPS=1 walks the batch in one group
-#define UINET_WALK_GROUPS 8
-#endif
-  const int groups = n >= 2 * kWalkGroupMin ? std::min(UINET_WALK_GROUPS, n / kWalkGroupMin) : 1;
-  if (groups > 1 && !c.side) {
-    rc = record_hip(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-    if (!rc) rc = record_hip(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
-    if (!rc) rc = record_hip(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
-    if (rc) return rc;
-  }
   for (int attempt = 0; attempt < 2; attempt++) {
-    rc = ctx_reserve(c, h_end, N, dev_layout(K, &d_sl, &d_ps, &d_ln, &d_sk, &d_sd, &d_st));
+    rc = ctx_reserve(c, h_end, N, 16 + walk_work(N, K).end);
     if (rc) return rc;
     uint8_t* d = c.d_buf;
-    rc = record_hip(hipMemsetAsync(d + d_st, 0, 8, c.stream));
-    if (!rc && groups > 1) rc = record_hip(hipEventRecord(c.fork, c.stream));
-    if (!rc && groups > 1) rc = record_hip(hipStreamWaitEvent(c.side, c.fork, 0));
-    for (int g = 0; g < groups && !rc; g++) {
-      const size_t i0 = N * (size_t)g / (size_t)groups, i1 = N * (size_t)(g + 1) / (size_t)groups;
-      const uint32_t ng = (uint32_t)(i1 - i0);
-      hipStream_t sg = (g & 1) ? c.side : c.stream;
-      rc = launch_walk_mbufs(reinterpret_cast<const uint64_t*>(dj) + i0,
-                             reinterpret_cast<const int32_t*>(dj + h_len) + i0,
-                             reinterpret_cast<const int32_t*>(dj + h_skip) + i0,
-                             seeded ? reinterpret_cast<const uint32_t*>(dj + h_seed) + i0 : nullptr,
-                             reinterpret_cast<const WalkRegionHost*>(dj + h_reg), (int)nreg, ng, K,
-                             (uint32_t)(i0 * K), lo_addr, kind == kWalkPseudo,
-                             reinterpret_cast<uint64_t*>(d) + i0 * K,
-                             reinterpret_cast<uint32_t*>(d + d_sl) + i0 * K,
-                             reinterpret_cast<uint32_t*>(d + d_ps) + i0,
-                             reinterpret_cast<uint32_t*>(d + d_ln) + i0,
-                             reinterpret_cast<uint32_t*>(d + d_sk) + i0,
-                             reinterpret_cast<uint32_t*>(d + d_sd) + i0,
-                             reinterpret_cast<uint32_t*>(d + d_st), sg);
-      // the group's rows are indexed from the list's row 0 (pkt_seg holds
-      // global row numbers)
-      if (!rc)
-        rc = launch_chains(reinterpret_cast<const void*>(lo_addr),
-                           reinterpret_cast<const uint64_t*>(d),
-                           reinterpret_cast<const uint32_t*>(d + d_sl),
-                           reinterpret_cast<const uint32_t*>(d + d_ps) + i0,
-                           reinterpret_cast<const uint32_t*>(d + d_ln) + i0,
-                           reinterpret_cast<const uint32_t*>(d + d_sk) + i0,
-                           seeded ? reinterpret_cast<const uint32_t*>(d + d_sd) + i0 : nullptr,
-                           static_cast<uint16_t*>(dout) + i0, ng, flags, 0, sg);
-    }
-    if (!rc && groups > 1) rc = record_hip(hipEventRecord(c.join, c.side));
-    if (!rc && groups > 1) rc = record_hip(hipStreamWaitEvent(c.stream, c.join, 0));
+    uint32_t* dstatus = reinterpret_cast<uint32_t*>(d);
+    rc = record_hip(hipMemsetAsync(dstatus, 0, 8, c.stream));
     if (!rc)
-      rc = record_hip(hipMemcpyAsync(h + h_st, d + d_st, 8, hipMemcpyDeviceToHost, c.stream));
-    if (rc && groups > 1) (void)hipStreamSynchronize(c.side);  // nothing left running
+      rc = launch_walk_fold(c, reinterpret_cast<const uint64_t*>(dj),
+                            reinterpret_cast<const int32_t*>(dj + h_len),
+                            reinterpret_cast<const int32_t*>(dj + h_skip),
+                            seeded ? reinterpret_cast<const uint32_t*>(dj + h_seed) : nullptr,
+                            reinterpret_cast<const WalkRegionHost*>(dj + h_reg), (int)nreg,
+                            lo_addr, N, K, kind == kWalkPseudo, d + 16, dstatus,
+                            static_cast<uint16_t*>(dout), flags);
+    if (!rc)
+      rc = record_hip(hipMemcpyAsync(h + h_st, dstatus, 8, hipMemcpyDeviceToHost, c.stream));
     const int wrc = ctx_wait(c);
     if (rc) return rc;
     if (wrc) return wrc;
     if (st[0]) return kFallback;  // a job the host walk must take
     const uint32_t longest = st[1];
-    // the next batch on this thread starts from this one's longest chain
-    uint32_t k2 = 4;
-    while (k2 < longest) k2 *= 2;
+    const uint32_t k2 = walk_k_for(longest);
     c.walk_k = k2;
     if (longest <= K) {
       for (int i = 0; i < n; i++) {
@@ -1077,6 +1120,95 @@ int run_jobs_made(int n, JobMaker make, JobFirst first, void* ctx, uint16_t* out
     return j.seed;
   }, [&](int i) { return ChainRef{first(ctx, i), 0x7fffffffL}; },  // chased like a whole chain
      kWalkSkip, true, [&](int i) { return make(ctx, i); });
+}
+
+int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* status) {
+  if (n <= 0 || !tuning().walk_device) return kFallback;
+  std::shared_lock<std::shared_mutex> g(g_reg_mu);
+  const size_t nreg_all = g_regions.size();
+  if (nreg_all == 0 || nreg_all > (size_t)kWalkRegionsMax) return kFallback;
+  Ctx* cp = nullptr;
+  int rc = ctx_current(&cp);
+  if (rc) return rc;
+  Ctx& c = *cp;
+  static const bool trace = getenv("UINET_CKSUM_TRACE_HOST") != nullptr;
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = trace ? clk::now() : clk::time_point();
+  const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const size_t N = (size_t)n, J = 2 * N;  // frames, jobs
+  // pinned: mbuf pointers u64[n] | regions | status u32[4] | verdicts u8[n]
+  const size_t h_reg = a16(8 * N), h_st = h_reg + a16(sizeof(WalkRegionHost) * nreg_all);
+  const size_t h_v = h_st + 16, h_end = h_v + a16(N);
+  // HBM: status | jobs (m u64, len i32, skip i32, seed u32) x 2n | plans | frames |
+  //      results u16[2n] | the walk's work area
+  const size_t d_jm = 16, d_jl = d_jm + a16(8 * J), d_js = d_jl + a16(4 * J);
+  const size_t d_jd = d_js + a16(4 * J), d_pl = d_jd + a16(4 * J);
+  const size_t d_fr = d_pl + a16(hook_plan_bytes(rx) * N), d_res = d_fr + a16(hook_frame_bytes() * N);
+  const size_t d_wa = d_res + a16(2 * J);
+  uint32_t K = c.walk_k ? c.walk_k : 4;
+  rc = ctx_reserve(c, h_end, N, d_wa + walk_work(J, K).end);
+  if (rc) return rc;
+  uint8_t* h = c.h_buf;
+  memcpy(h, mv, 8 * N);
+  size_t nreg = 0;
+  uint64_t lo = 0;
+  (void)walk_regions(reinterpret_cast<WalkRegionHost*>(h + h_reg), nreg_all, &nreg, &lo);
+  void* dhv = nullptr;
+  rc = record_hip(hipHostGetDevicePointer(&dhv, c.h_buf, 0));
+  if (rc) return rc;
+  const uint8_t* dh = static_cast<const uint8_t*>(dhv);
+  const WalkRegionHost* dregs = reinterpret_cast<const WalkRegionHost*>(dh + h_reg);
+  volatile uint32_t* st = reinterpret_cast<volatile uint32_t*>(h + h_st);
+  bool parsed = false;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    rc = ctx_reserve(c, h_end, N, d_wa + walk_work(J, K).end);
+    if (rc) return rc;
+    uint8_t* d = c.d_buf;
+    uint32_t* dstatus = reinterpret_cast<uint32_t*>(d);
+    uint64_t* jm = reinterpret_cast<uint64_t*>(d + d_jm);
+    int32_t* jl = reinterpret_cast<int32_t*>(d + d_jl);
+    int32_t* js = reinterpret_cast<int32_t*>(d + d_js);
+    uint32_t* jd = reinterpret_cast<uint32_t*>(d + d_jd);
+    rc = record_hip(hipMemsetAsync(dstatus, 0, 8, c.stream));
+    // the parse runs once; a second attempt (rows too short) walks its jobs again
+    // (ctx_reserve keeps the buffer's contents only when it does not grow it)
+    if (!rc && !parsed)
+      rc = launch_hook_parse(rx, reinterpret_cast<const uint64_t*>(dh), (uint32_t)n, l2len,
+                             dregs, (int)nreg, jm, jl, js, jd, d + d_pl, d + d_fr, dstatus,
+                             c.stream);
+    if (!rc)
+      rc = launch_walk_fold(c, jm, jl, js, jd, dregs, (int)nreg, lo, J, K, false, d + d_wa,
+                            dstatus, reinterpret_cast<uint16_t*>(d + d_res), 0);
+    if (!rc) {
+      void* dv = nullptr;
+      rc = record_hip(hipHostGetDevicePointer(&dv, h + h_v, 0));
+      if (!rc)
+        rc = launch_hook_apply(rx, d + d_pl, d + d_fr, reinterpret_cast<uint16_t*>(d + d_res),
+                               (uint32_t)n, K, dstatus, static_cast<uint8_t*>(dv), c.stream);
+    }
+    if (!rc) rc = record_hip(hipMemcpyAsync(h + h_st, dstatus, 8, hipMemcpyDeviceToHost, c.stream));
+    const int wrc = ctx_wait(c);
+    if (rc) return rc;
+    if (wrc) return wrc;
+    if (st[0]) return kFallback;  // the device view could not take a frame
+    const uint32_t longest = st[1];
+    const uint32_t k2 = walk_k_for(longest);
+    c.walk_k = k2;
+    if (longest <= K) {  // the apply step ran
+      if (status) memcpy(status, h + h_v, N);
+      note_device_walk();
+      if (trace)
+        fprintf(stderr, "uinet_cksum offload %s: n=%d on the device, K=%u | total %.3f ms\n",
+                rx ? "rx" : "tx", n, K,
+                std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+      return UINET_CKSUM_OK;
+    }
+    if (k2 > kWalkKMax || (uint64_t)J * k2 > 0xffffffffull) return kFallback;
+    // the rows must grow: the device buffer is reallocated, so parse again
+    if (walk_work(J, k2).end + d_wa > c.d_cap) parsed = false; else parsed = true;
+    K = k2;
+  }
+  return kFallback;
 }
 
 namespace {

@@ -110,4 +110,18 @@ int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* 
                       uint32_t* seg_len, uint32_t* pkt_seg, uint32_t* len_out, uint32_t* skip_out,
                       uint32_t* seed_out, uint32_t* status, hipStream_t stream);
 
+// Driver hooks on the device (cksum_hookdev.hip): k_hook_parse writes two jobs
+// per frame (jm / jl / js / jd: 2n entries) and its plan / frame records
+// (hook_plan_bytes / hook_frame_bytes each); k_hook_apply writes the verdicts
+// into the mbufs and st_out[n], unless status[0] is set or status[1] > K.
+size_t hook_plan_bytes(bool rx);
+size_t hook_frame_bytes();
+int launch_hook_parse(bool rx, const uint64_t* mv, uint32_t n, int l2len,
+                      const WalkRegionHost* regions, int nreg, uint64_t* jm, int32_t* jl,
+                      int32_t* js, uint32_t* jd, void* plans, void* frames, uint32_t* status,
+                      hipStream_t stream);
+int launch_hook_apply(bool rx, const void* plans, const void* frames, const uint16_t* res,
+                      uint32_t n, uint32_t K, const uint32_t* status, uint8_t* st_out,
+                      hipStream_t stream);
+
 }  // namespace uinet

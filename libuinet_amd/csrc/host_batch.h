@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+struct mbuf;  // the C ABI's opaque struct mbuf (include/uinet_cksum.h)
+
 namespace uinet {
 
 // struct m_hdr (sys/sys/mbuf.h:90-98) on amd64: M_HDR_PAD 6 (:82), 40 bytes.
@@ -68,6 +70,12 @@ int run_jobs(const Job* jobs, int n, uint16_t* out);
 typedef Job (*JobMaker)(void* ctx, int i);
 typedef const MbufHdr* (*JobFirst)(void* ctx, int i);
 int run_jobs_made(int n, JobMaker make, JobFirst first, void* ctx, uint16_t* out);
+
+// The RX (rx true) / TX hook of a batch whose mbufs and frames all lie in
+// registered memory, done on the device: parse, walk, fold and the verdicts
+// (cksum_hookdev.hip).  Returns 1 when it does not apply or the device view
+// could not take the batch (nothing was written), else a UINET_CKSUM_* code.
+int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* status);
 
 // Host CPU accounting of the batch entry points (uinet_cksum_host_cpu): a
 // CpuScope at each public host-batch entry adds the call's wall time, the

@@ -214,6 +214,41 @@ def test_device_walk_hooks(ora, torch_dev):
         assert np.array_equal(x, y)
 
 
+def test_device_hooks_fall_back_outside_regions(ora, torch_dev):
+    """A TX batch one of whose frames has its first mbuf's data outside the
+    registered regions: the device hook writes nothing and the host hook takes
+    the batch, with the oracle's results."""
+    from libuinet_amd.frames import FrameBatch, pkthdr_fields
+
+    a = FrameBatch(800, seed=12, ipv6=0.3)
+    b = FrameBatch(800, seed=12, ipv6=0.3)
+    other = rand_arena(1 << 16, 5)
+    first = int(a.tx.pkt_seg[3])
+    ln = int(a.tx.mbufs["m_len"][first])
+    src = int(a.tx.mbufs["m_data"][first]) - a.arena.ctypes.data
+    if 0 <= src <= a.arena.size - ln:  # move frame 3's first mbuf data out of the regions
+        other[:ln] = a.arena[src:src + ln]
+        a.tx.mbufs["m_data"][first] = other.ctypes.data
+        bf = int(b.tx.pkt_seg[3])
+        b.tx.mbufs["m_data"][bf] = other.ctypes.data + (1 << 15)
+        other[1 << 15:(1 << 15) + ln] = b.arena[src:src + ln]
+    else:  # headers in the mbuf itself: point at a copy outside
+        mb = a.tx.mbufs.view(np.uint8).reshape(-1, 256)
+        off = int(a.tx.mbufs["m_data"][first]) - a.tx.mbufs.ctypes.data - 256 * first
+        other[:ln] = mb[first, off:off + ln]
+        a.tx.mbufs["m_data"][first] = other.ctypes.data
+        other[1 << 15:(1 << 15) + ln] = mb[first, off:off + ln]
+        b.tx.mbufs["m_data"][int(b.tx.pkt_seg[3])] = other.ctypes.data + (1 << 15)
+    with registered(a.arena, a.tx.mbufs):
+        st, nw = walks(lambda: u.tx_offload(a.tx.heads))
+    assert nw == 0
+    assert np.array_equal(st, ora.tx_offload(b.tx.heads))
+    assert np.array_equal(a.arena, b.arena)
+    assert np.array_equal(other[:ln], other[1 << 15:(1 << 15) + ln])
+    for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
+        assert np.array_equal(x, y)
+
+
 def test_host_cpu_counters(arena):
     """uinet_cksum_host_cpu counts calls, packets, wall and CPU time on the
     calling thread, and resets."""

@@ -119,6 +119,8 @@ def test_fuzz_device_entry_points(ora):
     try:
         for t in range(TRIALS):
             _trial(torch, ora, arena, d_arena, t)
+            if t % 1000 == 999:
+                print(f"fuzz: {t + 1} trials", flush=True)
         print(f"fuzz: {TRIALS} trials, {_trial.packets} packets")
     finally:
         for k, v in DEFAULTS.items():
@@ -193,6 +195,8 @@ def test_fuzz_host_batches(ora):
     try:
         for t in range(max(1, TRIALS // 3)):
             packets += _host_trial(ora, arena, t)
+            if t % 200 == 199:  # long hunts: a sign of life every few seconds
+                print(f"host fuzz: {t + 1} trials", flush=True)
         print(f"host fuzz: {max(1, TRIALS // 3)} trials, {packets} packets")
     finally:
         for k, v in HOST_DEFAULTS.items():
@@ -262,6 +266,8 @@ def test_fuzz_offload_hooks(ora):
             for x, y in zip(pkthdr_fields(rx_a), pkthdr_fields(rx_b)):
                 assert np.array_equal(x, y), ctx + f" corrupt={corrupt} (RX marks)"
             frames += n
+            if t % 50 == 49:
+                print(f"offload fuzz: {t + 1} trials", flush=True)
         print(f"offload fuzz: {max(1, TRIALS // 10)} trials, {frames} frames each way")
     finally:
         for k, v in HOST_DEFAULTS.items():
