@@ -289,7 +289,11 @@ int uinet_cksum_unregister_host(void *base);
 /* -1 = parse an Ethernet header (14 bytes, 18 with one 802.1Q tag; type    */
 /* 0x0800 or 0x86dd), >= 0 = the IP header is there and its version nibble  */
 /* tells IPv4 from IPv6 (ip_output's view: 0).  One GPU batch per call;     */
-/* status[i] (may be NULL) receives UINET_RX_* / UINET_TX_* bits.           */
+/* status[i] (may be NULL) receives UINET_RX_* / UINET_TX_* bits.  When the */
+/* mbufs and frames all lie in registered memory (2c) and "walk_device" is  */
+/* 1, the whole hook runs on the GPU -- header parse, walk, fold and the    */
+/* writes into the mbufs -- and the host only copies the mbuf pointers;     */
+/* otherwise the host pool parses and walks.  Same results either way.      */
 /* ------------------------------------------------------------------------ */
 
 #define UINET_RX_IPV4    0x01 /* IPv4 header parsed */

@@ -20,3 +20,8 @@ for r in 1 2 3; do
   step host_cpu_$r 600 python -u tests/perf/host_cpu.py
 done
 echo "== done"
+# (round 5, r05i and later) where a device hook batch's time goes
+if [ -n "${HOOK_TRACE:-}" ]; then
+step hook_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/hook_trace" -o run --output-format csv -- python3 tests/perf/host_cpu.py --work hooks --paths dev_walk --threads 1 --reps 3
+echo "== done (hook trace)"
+fi
