@@ -60,6 +60,9 @@ def parse():
                     "6-B (uinet_cksum_chains32 / uinet_cksum_spans32) descriptors")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--host-offload", choices=["auto", "off"], default="auto",
+                    help="N = 1: also fold the batch as host-resident registered mbufs "
+                    "(device walk) and report its host CPU per 1,000 packets")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc")
     ap.add_argument("--scaling-ref", default=os.path.join(REPO, "profiles", "scaling_ref.json"),
@@ -381,15 +384,23 @@ def reference_results(cfg: str, w, threads: int):
     return kind, np.ascontiguousarray(out, dtype=np.uint16)
 
 
-def cpu_baseline(cfg: str, w, gpu_out, threads: int):
+def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
     """The reference's scalar in_cksum_skip / in_cksum_pseudo_header over the same
-    bytes as host mbufs; returns the cpu_baseline object (and checks parity)."""
+    bytes as host mbufs; returns the cpu_baseline object (and checks parity).
+    ``keep`` (a dict) receives the host mbufs and call arguments for
+    host_offload_line."""
     import oracle
     from libuinet_amd.mbuf import MbufChains
 
+    from libuinet_amd.mbuf import aligned_empty
+
     kind = "reference" if oracle.have_reference() else "port"
     R = oracle.Reference() if kind == "reference" else None
-    host = w["arena"].cpu().numpy()
+    # page-aligned, so host_offload_line can register it with the engine
+    src = w["arena"].cpu().numpy()
+    host = aligned_empty(src.size)
+    host[:] = src
+    del src
     try:
         allowed = sorted(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
@@ -419,6 +430,9 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
         args = (ch.heads, w["length"], 0)
         timer = (lambda nt, cp, r: R.time_skip(*args, nthreads=nt, cpus=cp, reps=r)) if R else None
         port = lambda: oracle.Oracle().skip_batch(*args, nthreads=threads)  # noqa: E731
+    if keep is not None:
+        keep.update(host=host, ch=ch, args=args,
+                    pseudo=cfg in ("5", "5tso"))
     gib = w["bytes"] / 2**30
     runs, spread = {}, {}
     if timer is not None:
@@ -481,6 +495,49 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int):
         "all_cores_from": best_all,
         "mask_cpus": len(allowed),
         "bit_identical_to_gpu": parity,
+    }
+
+
+def host_offload_line(keep, n: int, nbytes: int, gpu_out, ref_1t_s, reps: int = 5):
+    """The benchmarked batch once more as HOST-resident mbufs, the way libuinet
+    holds them: packet bytes and mbufs registered with the engine
+    (uinet_cksum_register_host), folded through the host-mbuf batch API --
+    the GPU walks the chains and reads the bytes over PCIe.  Reports wall time
+    and the host CPU the call cost (uinet_cksum_host_cpu: calling thread +
+    engine pool helpers) per 1,000 packets, beside the reference's 1-thread
+    pass over the same mbufs (a scalar loop: its CPU time is its wall time).
+    Never `value`; SURVEY.md section 7 step 7 / VERDICT r04 item 1."""
+    import libuinet_amd as u
+
+    ch, args = keep["ch"], keep["args"]
+    fn = u.in_cksum_pseudo_header_batch if keep["pseudo"] else u.in_cksum_skip_batch
+    bufs = [keep["host"], ch.mbufs]
+    for b in bufs:
+        u.register_host(b)
+    try:
+        fn(*args)  # warm: staging, walk row size
+        rows = []
+        for _ in range(reps):
+            u.host_cpu(reset=True)
+            t0 = time.perf_counter()
+            out = fn(*args)
+            rows.append((time.perf_counter() - t0, u.host_cpu(reset=True), out))
+    finally:
+        for b in bufs:
+            u.unregister_host(b)
+    rows.sort(key=lambda r: r[0])
+    wall, st, out = rows[len(rows) // 2]
+    k = n / 1000
+    return {
+        "what": "the benchmarked batch as host mbufs in registered memory, through the host-mbuf "
+                "batch API (the GPU walks the chains over PCIe); median of %d calls" % reps,
+        "wall_ms": round(wall * 1e3, 3),
+        "gibs": round(nbytes / wall / 2**30, 2),
+        "host_cpu_us_per_1k_pkts": round(st["cpu_ns"] / 1e3 / k, 3),
+        "device_walked": bool(st["device_walks"] == st["calls"]),
+        "reference_1thread_ms": round(ref_1t_s * 1e3, 3) if ref_1t_s else None,
+        "reference_1thread_cpu_us_per_1k_pkts": round(ref_1t_s * 1e6 / k, 3) if ref_1t_s else None,
+        "bit_identical": bool(all(np.array_equal(r[2], gpu_out) for r in rows)),
     }
 
 
@@ -736,8 +793,16 @@ def run(args, distributed: bool, wd):
     if world == 1 and rank == 0 and args.cpu_baseline == "auto":
         torch.cuda.synchronize()
         gpu_out = outs[(K - 1) % NBUF].cpu().view(torch.int16).numpy().view(np.uint16)
-        result["cpu_baseline"] = cpu_baseline(args.config, w, gpu_out, args.cpu_threads)
+        keep = {}
+        result["cpu_baseline"] = cpu_baseline(args.config, w, gpu_out, args.cpu_threads, keep)
         result["bit_identical"] = result["cpu_baseline"]["bit_identical_to_gpu"]
+        if args.host_offload == "auto":
+            try:
+                t1 = result["cpu_baseline"].get("one_thread_gibs")
+                ref_1t = w["bytes"] / 2**30 / t1 if t1 else None
+                result["host_resident_cpu"] = host_offload_line(keep, n, w["bytes"], gpu_out, ref_1t)
+            except Exception as e:  # a report, never the measurement: say what failed
+                result["host_resident_cpu"] = {"error": f"{type(e).__name__}: {e}"}
         result["parity"] = {"packets": n, "against": result["cpu_baseline"]["kind"],
                             "how": "the last timed step's results vs the reference's "
                                    "in_cksum_* over the same bytes as host mbufs"}

@@ -782,6 +782,7 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
   uint32_t K = c.walk_k ? c.walk_k : 4;
   const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const size_t N = (size_t)n;
+  if ((uint64_t)N * K > 0xffffffffull) return kFallback;  // rows indexed by u32
   // pinned: heads u64 | len i32 | skip i32 | seed u32 | regions | status u32[2]
   const size_t h_len = a16(8 * N), h_skip = h_len + a16(4 * N), h_seed = h_skip + a16(4 * N);
   const size_t h_reg = h_seed + (seeded ? a16(4 * N) : 0);
@@ -1146,6 +1147,7 @@ int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* 
   const size_t d_fr = d_pl + a16(hook_plan_bytes(rx) * N), d_res = d_fr + a16(hook_frame_bytes() * N);
   const size_t d_wa = d_res + a16(2 * J);
   uint32_t K = c.walk_k ? c.walk_k : 4;
+  if ((uint64_t)J * K > 0xffffffffull) return kFallback;  // rows indexed by u32
   rc = ctx_reserve(c, h_end, N, d_wa + walk_work(J, K).end);
   if (rc) return rc;
   uint8_t* h = c.h_buf;

@@ -102,3 +102,16 @@ def test_bench_nccl_world1_rccl_gather(tmp_path, torch_dev):
     assert d["config"]["launcher"] == "torch.distributed.run"
     got = np.load(path)
     np.testing.assert_array_equal(got, _want_config2(n, 1))
+
+
+def test_bench_n1_host_resident_cpu_line(torch_dev):
+    """The N = 1 line folds its batch once more as host mbufs in registered
+    memory (the GPU walks the chains) and reports the host CPU that cost,
+    beside the reference's one-thread pass; bit-identical to the timed step."""
+    d = _bench([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--packets", "65536"],
+               {}, timeout=300)
+    h = d["host_resident_cpu"]
+    assert "error" not in h, h
+    assert h["bit_identical"] is True and h["device_walked"] is True
+    assert h["wall_ms"] > 0 and h["host_cpu_us_per_1k_pkts"] > 0
+    assert h["reference_1thread_cpu_us_per_1k_pkts"] > 0
