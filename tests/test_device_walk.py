@@ -220,8 +220,8 @@ def test_device_hooks_fall_back_outside_regions(ora, torch_dev):
     the batch, with the oracle's results."""
     from libuinet_amd.frames import FrameBatch, pkthdr_fields
 
-    a = FrameBatch(800, seed=12, ipv6=0.3)
-    b = FrameBatch(800, seed=12, ipv6=0.3)
+    a = FrameBatch(2500, seed=12, ipv6=0.3)  # >= 2,048 frames: the device hook's size
+    b = FrameBatch(2500, seed=12, ipv6=0.3)
     other = rand_arena(1 << 16, 5)
     first = int(a.tx.pkt_seg[3])
     ln = int(a.tx.mbufs["m_len"][first])
@@ -245,6 +245,29 @@ def test_device_hooks_fall_back_outside_regions(ora, torch_dev):
     assert np.array_equal(st, ora.tx_offload(b.tx.heads))
     assert np.array_equal(a.arena, b.arena)
     assert np.array_equal(other[:ln], other[1 << 15:(1 << 15) + ln])
+    for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
+        assert np.array_equal(x, y)
+
+
+def test_small_batches_are_staged(ora, arena, torch_dev):
+    """Over registered memory, batches of at most 128 packets and hook batches
+    below 2,048 frames are staged (one launch out of mapped memory answers
+    sooner, profiles/r05/r05k/); results equal the oracle's either way."""
+    from libuinet_amd.frames import FrameBatch, pkthdr_fields
+
+    rng = np.random.default_rng(8)
+    ch, _, _ = chains(rng, arena, 129)
+    with registered(arena, ch.mbufs):
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads[:128], 1 << 20, 0))
+        assert nw == 0 and np.array_equal(got, ora.skip_batch(ch.heads[:128], 1 << 20, 0))
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 20, 0))
+        assert nw == 1 and np.array_equal(got, ora.skip_batch(ch.heads, 1 << 20, 0))
+    a = FrameBatch(2047, seed=13)
+    b = FrameBatch(2047, seed=13)
+    with registered(a.arena, a.tx.mbufs):
+        st, nw = walks(lambda: u.tx_offload(a.tx.heads))
+    assert nw == 0 and np.array_equal(st, ora.tx_offload(b.tx.heads))
+    assert np.array_equal(a.arena, b.arena)
     for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
         assert np.array_equal(x, y)
 

@@ -220,7 +220,9 @@ def test_fuzz_offload_hooks(ora):
             u.set_tuning("host_threads", int(rng.choice([1, 3, 16])))
             u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
             u.set_tuning("walk_device", int(rng.integers(0, 2)))
-            n = int(rng.choice([1, 2, int(rng.integers(1, 1500))]))
+            # batches of 2,048 frames and more take the device hook when their
+            # mbufs are registered (cksum_hookdev.hip); smaller ones the host hook
+            n = int(rng.choice([1, 2, int(rng.integers(1, 1500)), int(rng.integers(2048, 3000))]))
             l2 = bool(rng.integers(0, 2))
             l2len = -1 if l2 else 0
             ipv6 = float(rng.choice([0.0, 0.3, 1.0]))
