@@ -101,6 +101,16 @@ def test_host_batch_multi(torch_dev, ora, devices):
     u.register_host(lay["arena"])  # zero-copy shards: every byte in registered memory
     try:
         got = u.in_cksum_skip_batch_multi(devices, ch.heads, lay["lens"], 20)
+        np.testing.assert_array_equal(got, want)
+        # the mbufs registered too: every shard's chains walked by its device
+        u.register_host(ch.mbufs)
+        try:
+            w0 = u.host_cpu()["device_walks"]
+            got = u.in_cksum_skip_batch_multi(devices, ch.heads, lay["lens"], 20)
+            if len(devices) == 1:  # one shard: it runs on the calling thread
+                assert u.host_cpu()["device_walks"] == w0 + 1
+        finally:
+            u.unregister_host(ch.mbufs)
     finally:
         u.unregister_host(lay["arena"])
     np.testing.assert_array_equal(got, want)
