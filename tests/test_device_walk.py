@@ -285,3 +285,59 @@ def test_host_cpu_counters(arena):
     assert st["wall_ns"] > 0 and st["caller_cpu_ns"] > 0
     assert st["cpu_ns"] == st["caller_cpu_ns"] + st["helper_cpu_ns"]
     assert u.host_cpu()["calls"] == 0
+
+
+def test_device_paths_concurrent_threads(ora, arena, torch_dev):
+    """An RX thread and a TX thread (libuinet's per-interface kthreads,
+    uinet_if_netmap.c:1648-1665) and a host-batch thread calling the device
+    paths at once, each on its own registered batch: every call equals the
+    oracle (each thread has its own stream and staging; regions are shared)."""
+    import threading
+
+    from libuinet_amd.frames import FrameBatch
+
+    rng = np.random.default_rng(9)
+    ch, _, _ = chains(rng, arena, 3000)
+    want_skip = ora.skip_batch(ch.heads, 1 << 20, 0)
+    tx_a, tx_b = FrameBatch(2500, seed=21, ipv6=0.3), FrameBatch(2500, seed=21, ipv6=0.3)
+    want_tx = ora.tx_offload(tx_b.tx.heads)
+    rx_src = FrameBatch(2500, seed=22, ipv6=0.3)
+    rx, rx_arena, _ = rx_src.rx(seed=2, corrupt=0.05)
+    rx_ref, _, _ = FrameBatch(2500, seed=22, ipv6=0.3).rx(seed=2, corrupt=0.05)
+    want_rx = ora.rx_offload(rx_ref.heads)
+    errors = []
+
+    def tx_loop():
+        try:
+            for _ in range(10):
+                # re-armed flags; the sums of a repeat differ (their fields now
+                # hold final sums), the per-frame status does not
+                tx_a.set_tx_flags()
+                st = u.tx_offload(tx_a.tx.heads)
+                assert np.array_equal(st, want_tx)
+        except Exception as e:  # reported below
+            errors.append(("tx", e))
+
+    def rx_loop():
+        try:
+            for _ in range(10):
+                rx.mbufs["csum_flags"][:] = 0
+                rx.mbufs["csum_data"][:] = 0
+                assert np.array_equal(u.rx_offload(rx.heads), want_rx)
+        except Exception as e:
+            errors.append(("rx", e))
+
+    def skip_loop():
+        try:
+            for _ in range(10):
+                assert np.array_equal(u.in_cksum_skip_batch(ch.heads, 1 << 20, 0), want_skip)
+        except Exception as e:
+            errors.append(("skip", e))
+
+    with registered(arena, ch.mbufs, tx_a.arena, tx_a.tx.mbufs, rx_arena, rx.mbufs):
+        ts = [threading.Thread(target=f) for f in (tx_loop, rx_loop, skip_loop)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=100)
+    assert not errors, errors
