@@ -1197,13 +1197,9 @@ int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* 
     if (!rc)
       rc = launch_walk_fold(c, jm, jl, js, jd, dregs, (int)nreg, lo, J, K, false, d + d_wa,
                             dstatus, reinterpret_cast<uint16_t*>(d + d_res), 0);
-    if (!rc) {
-      void* dv = nullptr;
-      rc = record_hip(hipHostGetDevicePointer(&dv, h + h_v, 0));
-      if (!rc)
-        rc = launch_hook_apply(rx, d + d_pl, d + d_fr, reinterpret_cast<uint16_t*>(d + d_res),
-                               (uint32_t)n, K, dstatus, static_cast<uint8_t*>(dv), c.stream);
-    }
+    if (!rc)
+      rc = launch_hook_apply(rx, d + d_pl, d + d_fr, reinterpret_cast<uint16_t*>(d + d_res),
+                             (uint32_t)n, K, dstatus, const_cast<uint8_t*>(dh) + h_v, c.stream);
     if (!rc) rc = record_hip(hipMemcpyAsync(h + h_st, dstatus, 8, hipMemcpyDeviceToHost, c.stream));
     const int wrc = ctx_wait(c);
     if (rc) return rc;
