@@ -41,12 +41,14 @@ __device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
 }
 
-// Two lanes per packet.  The walk's rate is the number of PCIe reads in
-// flight over their latency, so what a hop costs is its requests: lanes 2k
-// and 2k + 1 load the two 16-B halves of the header's first 32 bytes in ONE
-// instruction, which the coalescer issues as one request for the line (one
-// lane loading both halves issues two), then swap halves over DPP.  Both
-// lanes of a pair follow the same chain, so their control flow is identical.
+// Two lanes per packet: lanes 2k and 2k + 1 load the two 16-B halves of the
+// header's first 32 bytes in ONE instruction, which the coalescer issues as
+// one request for the line (one lane loading both halves issues two), then
+// swap halves over DPP.  Both lanes of a pair follow the same chain, so their
+// control flow is identical.  What bounds the walk is the host link, not the
+// requests: every hop costs L2 a 128-B line read over PCIe for 32 useful
+// bytes, and the walk moves those lines at ~40 GB/s, the rate the fold reads
+// packet bytes at (k_walk_mbufs; profiles/r05/r05p-r05r).
 __global__ __launch_bounds__(256) void k_walk_mbufs(
     const uint64_t* __restrict__ heads, const int32_t* __restrict__ jlen,
     const int32_t* __restrict__ jskip, const uint32_t* __restrict__ jseed,
