@@ -197,7 +197,76 @@ static int cold(int n) {
   return 0;
 }
 
+// Independent (not chained) 32-B reads at random 256-B slots: lanes 2k and
+// 2k + 1 read the two 16-B halves of slot hash(k), the device walk's access
+// shape without its dependency -- the link's rate for scattered line reads.
+__global__ __launch_bounds__(256) void k_read_slots(const uint4* __restrict__ p, uint64_t nslot,
+                                                    uint64_t reads, uint32_t* __restrict__ sink) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (uint64_t i = tid; i < 2 * reads; i += nthr) {
+    uint64_t h = (i >> 1) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    const uint64_t slot = h % nslot;
+    const uint4 v = p[slot * 16 + (i & 1)];
+    acc += v.x + v.y + v.z + v.w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// `hbm_read host BYTES`: the same reads over registered host memory (the
+// zero-copy and device-walk paths' source), through its device alias, beside
+// a hipMemcpy of the buffer to HBM: the PCIe ceiling the host-resident paths
+// are measured against.
+static int host(uint64_t bytes) {
+  const uint64_t n16 = bytes / 16;
+  void* h = nullptr;
+  if (posix_memalign(&h, 4096, bytes)) return 1;
+  memset(h, 0x5a, bytes);
+  CK(hipHostRegister(h, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  uint4* p;
+  CK(hipHostGetDevicePointer((void**)&p, h, 0));
+  uint4* d;
+  uint32_t* sink;
+  CK(hipMalloc(&d, bytes));
+  CK(hipMalloc(&sink, 64));
+  printf("{\"bytes\": %llu, \"memory\": \"registered host\", \"results\": [\n",
+         (unsigned long long)bytes);
+  bool first = true;
+  auto report = [&](const char* name, int grid, float ms, double moved, double n_reads) {
+    printf("%s {\"kernel\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"GBps\": %.2f, \"Mreads_per_s\": %.1f}\n",
+           first ? "" : ",", name, grid, ms, moved / (ms * 1e-3) / 1e9,
+           n_reads / (ms * 1e-3) / 1e6);
+    first = false;
+    fflush(stdout);
+  };
+  report("hipMemcpy_h2d", 0, time_it([&] { CK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice)); }, 5),
+         (double)bytes, 0);
+  const int grids[] = {1024, 4096, 16384};
+  for (int g : grids) {
+    report("stride_u4", g, time_it([&] { k_read<4, false><<<g, 256>>>(p, n16, sink); }, 5),
+           (double)bytes, (double)bytes / 64);
+    report("stride_u8", g, time_it([&] { k_read<8, false><<<g, 256>>>(p, n16, sink); }, 5),
+           (double)bytes, (double)bytes / 64);
+  }
+  const uint64_t tiles = (n16 + 1023) / 1024;
+  report("tile_u4", (int)tiles,
+         time_it([&] { k_read_tile<4, false><<<(int)tiles, 256>>>(p, n16, sink); }, 5),
+         (double)bytes, (double)bytes / 64);
+  const uint64_t nslot = bytes / 256, reads = 4u << 20;
+  for (int g : grids)
+    report("slots_32B", g,
+           time_it([&] { k_read_slots<<<g, 256>>>(p, nslot, reads, sink); }, 5),
+           (double)reads * 32, (double)reads);
+  printf("]}\n");
+  CK(hipHostUnregister(h));
+  free(h);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 2 && !strcmp(argv[1], "host")) return host(strtoull(argv[2], 0, 0));
   if (argc > 2 && !strcmp(argv[1], "cold")) return cold(atoi(argv[2]));
   if (argc > 3 && !strcmp(argv[1], "cold_valu")) {
     const int k = atoi(argv[3]), n = atoi(argv[2]);
