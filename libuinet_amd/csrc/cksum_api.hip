@@ -772,6 +772,23 @@ uint32_t walk_k_for(uint32_t longest) {
   return k;
 }
 
+// Whether the first, middle and last chains of a batch start in registered
+// memory.  When only the packet bytes are registered (the zero-copy setup),
+// the device paths would launch their kernels only to find every mbuf
+// unmapped and hand the batch back; this sends it to the host walk first.
+// (A batch that passes and still holds an unregistered mbuf is caught by the
+// kernels' status word as before.)  Called with g_reg_mu held.
+template <typename HeadAt>
+bool heads_registered(int n, const HeadAt& head_at) {
+  const int idx[3] = {0, n / 2, n - 1};
+  for (int i : idx) {
+    const uint8_t* m = reinterpret_cast<const uint8_t*>(head_at(i));
+    uint64_t dev;
+    if (m && !device_addr(g_regions, m, 32, &dev)) return false;
+  }
+  return true;
+}
+
 // job(i) -> Job (the in_cksum_skip form; len and skip as the caller gave
 // them).  Returns kFallback (nothing delivered) when the batch must take the
 // host walk.  Called with g_reg_mu held (shared) and at least one region.
@@ -783,6 +800,7 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
   const clk::time_point t0 = trace ? clk::now() : clk::time_point();
   const size_t nreg_all = g_regions.size();
   if (nreg_all == 0 || nreg_all > (size_t)kWalkRegionsMax) return kFallback;
+  if (!heads_registered(n, [&](int i) { return job(i).m; })) return kFallback;
   uint32_t K = c.walk_k ? c.walk_k : 4;
   const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const size_t N = (size_t)n;
@@ -1144,6 +1162,7 @@ int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* 
   std::shared_lock<std::shared_mutex> g(g_reg_mu);
   const size_t nreg_all = g_regions.size();
   if (nreg_all == 0 || nreg_all > (size_t)kWalkRegionsMax) return kFallback;
+  if (!heads_registered(n, [&](int i) { return mv[i]; })) return kFallback;
   Ctx* cp = nullptr;
   int rc = ctx_current(&cp);
   if (rc) return rc;
