@@ -109,6 +109,14 @@ struct DevView {
     }
     return read_slow(off, dst, n);
   }
+  __device__ const uint8_t* bytes(int off, uint8_t* tmp, int n, int* got) const {
+    if (off >= 0 && off + n <= win_n) {
+      *got = n;
+      return win + off;
+    }
+    *got = read_slow(off, tmp, n);
+    return tmp;
+  }
   __device__ int read_slow(int off, uint8_t* dst, int n) const {
     int got = 0;
     uint64_t cur = m, dcur = dm, data = 0;

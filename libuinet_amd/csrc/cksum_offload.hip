@@ -65,6 +65,14 @@ struct HostView {
   MbufHdr* m;
   uint64_t addr() const { return reinterpret_cast<uint64_t>(m); }
   int read(int off, uint8_t* dst, int n) const { return chain_read(m, off, dst, n); }
+  const uint8_t* bytes(int off, uint8_t* tmp, int n, int* got) const {
+    if (m && off >= 0 && m->m_len > 0 && off + n <= m->m_len) {  // in the first mbuf
+      *got = n;
+      return reinterpret_cast<const uint8_t*>(m->m_data) + off;
+    }
+    *got = chain_read(m, off, tmp, n);
+    return tmp;
+  }
   long length() const { return chain_len(m); }
   int m_flags() const { return m->m_flags; }
   int m_len() const { return m->m_len; }

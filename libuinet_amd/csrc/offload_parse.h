@@ -5,6 +5,10 @@
 // Every function reads the packet through a View:
 //   uint64_t addr()                 the head mbuf's address (0 = none)
 //   int read(off, dst, n)           up to n bytes at chain offset off (count read)
+//   const uint8_t* bytes(off, tmp, n, &got)
+//                                   the same bytes, in place when the view holds
+//                                   them contiguously (first mbuf / window), else
+//                                   read into tmp
 //   long length()                   the chain's byte count
 //   int m_flags(), m_len()          the first mbuf's m_flags / m_len
 //   int csum_flags(), csum_data()   its m_pkthdr.csum_flags / csum_data
@@ -95,13 +99,15 @@ struct TxPlan {
 // the header sits at l2len and its version nibble tells.
 template <class V>
 UINET_HD int l3_locate(const V& v, int l2len, int* l3) {
-  uint8_t b[18];
+  uint8_t t[18];
+  int got = 0;
   if (l2len >= 0) {
     *l3 = l2len;
-    if (v.read(l2len, b, 1) < 1) return 0;
+    const uint8_t* b = v.bytes(l2len, t, 1, &got);
+    if (got < 1) return 0;
     return (b[0] >> 4) == 4 ? 4 : (b[0] >> 4) == 6 ? 6 : 0;
   }
-  const int got = v.read(0, b, 18);
+  const uint8_t* b = v.bytes(0, t, 18, &got);
   if (got < 14) return 0;
   uint16_t et = be16(b + 12);
   *l3 = 14;
@@ -113,13 +119,20 @@ UINET_HD int l3_locate(const V& v, int l2len, int* l3) {
   return et == 0x0800 ? 4 : et == 0x86dd ? 6 : 0;
 }
 
+// The header, and with want_l4 the first 8 bytes after it (RX's UDP checks;
+// TX never looks at them).  Reads no byte it does not use: past the first
+// mbuf the device view pays two more host lines per frame (the next mbuf's
+// header and data), so the header length is read first.
 template <class V>
-UINET_HD bool parse_ip4(const V& v, int l3, Ip4* o) {
-  uint8_t b[60 + 8];
-  const int got = v.read(l3, b, 60 + 8);
+UINET_HD bool parse_ip4(const V& v, int l3, Ip4* o, bool want_l4) {
+  uint8_t t[60 + 8];
+  int got = 0;
+  const uint8_t* b = v.bytes(l3, t, 20, &got);
   if (got < 20 || (b[0] >> 4) != 4) return false;
   const int hl = (b[0] & 15) * 4;
-  if (hl < 20 || got < hl) return false;
+  if (hl < 20) return false;
+  if (hl + (want_l4 ? 8 : 0) > 20) b = v.bytes(l3, t, hl + (want_l4 ? 8 : 0), &got);
+  if (got < hl) return false;
   o->l3 = l3;
   o->hl = hl;
   o->ip_len = be16(b + 2);
@@ -133,9 +146,10 @@ UINET_HD bool parse_ip4(const V& v, int l3, Ip4* o) {
 }
 
 template <class V>
-UINET_HD bool parse_ip6(const V& v, int l3, Ip6* o) {
-  uint8_t b[40 + 8];
-  const int got = v.read(l3, b, 40 + 8);
+UINET_HD bool parse_ip6(const V& v, int l3, Ip6* o, bool want_l4) {
+  uint8_t t[40 + 8];
+  int got = 0;
+  const uint8_t* b = v.bytes(l3, t, 40 + (want_l4 ? 8 : 0), &got);
   if (got < 40 || (b[0] >> 4) != 6) return false;
   o->l3 = l3;
   o->plen = be16(b + 4);
@@ -180,8 +194,11 @@ UINET_HD int ip6_walk(const V& v, const Ip6& ip, bool rx, int* off, int* nxt) {
       *nxt = x;
       return x == 44 ? 0 : 1;
     }
-    uint8_t e[4];
-    if (o + 8 > 40 + ip.plen || v.read(ip.l3 + o, e, 4) < 4) return -1;
+    if (o + 8 > 40 + ip.plen) return -1;
+    uint8_t t[4];
+    int got = 0;
+    const uint8_t* e = v.bytes(ip.l3 + o, t, 4, &got);
+    if (got < 4) return -1;
     if (rx && x == 43 && e[3] != 0) return -1;  // segments left: route6.c:99-105
     x = e[0];
     o += (e[1] + 1) * 8;
@@ -221,8 +238,9 @@ UINET_HD PJob rx6_job(const V& v, const Ip6& ip, uint8_t* st) {
     uint8_t u[8];
     const uint8_t* uh = ip.l4;
     if (off != 40) {
-      if (v.read(ip.l3 + off, u, 8) < 8) return none;
-      uh = u;
+      int got = 0;
+      uh = v.bytes(ip.l3 + off, u, 8, &got);
+      if (got < 8) return none;
     } else if (ip.l4_have < 8) {
       return none;
     }
@@ -248,7 +266,7 @@ UINET_HD PJob rx_parse(const V& v, int l2len, RxPlan& p, PJob* l4) {
   const int ver = v.addr() ? l3_locate(v, l2len, &l3) : 0;
   if (ver == 6) {
     Ip6 ip6;
-    if (!parse_ip6(v, l3, &ip6)) return none;
+    if (!parse_ip6(v, l3, &ip6, true)) return none;
     p.st |= UINET_RX_IPV6;
     const PJob j = rx6_job(v, ip6, &p.st);
     if (j.m) {
@@ -258,7 +276,7 @@ UINET_HD PJob rx_parse(const V& v, int l2len, RxPlan& p, PJob* l4) {
     return none;
   }
   Ip4 ip;
-  if (ver != 4 || !parse_ip4(v, l3, &ip)) return none;
+  if (ver != 4 || !parse_ip4(v, l3, &ip, true)) return none;
   p.st |= UINET_RX_IPV4;
   p.ip_job = true;  // in_cksum(m, hlen) over the header (ip_input.c:463-467)
   const PJob hdr{v.addr(), ip.l3 + ip.hl, ip.l3, 0u};
@@ -308,7 +326,7 @@ UINET_HD PJob tx_parse(V& v, int l2len, TxPlan& p, PJob* l4) {
     // field holds the final destination.
     Ip6 ip6;
     int off = 40, nxt = 0;
-    if (!(fl & (kCsumTcpIpv6 | kCsumUdpIpv6)) || !parse_ip6(v, l3, &ip6) || ip6.plen == 0 ||
+    if (!(fl & (kCsumTcpIpv6 | kCsumUdpIpv6)) || !parse_ip6(v, l3, &ip6, false) || ip6.plen == 0 ||
         ip6_walk(v, ip6, false, &off, &nxt) != 1) {
       p.st = UINET_TX_SKIP;
       return none;
@@ -322,7 +340,7 @@ UINET_HD PJob tx_parse(V& v, int l2len, TxPlan& p, PJob* l4) {
     return none;
   }
   Ip4 ip;
-  if (ver != 4 || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) || !parse_ip4(v, l3, &ip)) {
+  if (ver != 4 || !(fl & (kCsumIp | kCsumTcp | kCsumUdp)) || !parse_ip4(v, l3, &ip, false)) {
     p.st = UINET_TX_SKIP;
     return none;
   }

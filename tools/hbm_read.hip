@@ -215,6 +215,30 @@ __global__ __launch_bounds__(256) void k_read_slots(const uint4* __restrict__ p,
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// One lane per random 256-B slot, loading C consecutive 16-B chunks of its
+// first 128-B line with C independent loads issued back to back (the hook
+// parse's window copy): do concurrent misses to one line of host memory
+// merge in L2, or does each become a read over the link?
+template <int C>
+__global__ __launch_bounds__(256) void k_read_line_chunks(const uint4* __restrict__ p,
+                                                          uint64_t nslot, uint64_t lines,
+                                                          uint32_t* __restrict__ sink) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (uint64_t i = tid; i < lines; i += nthr) {
+    uint64_t h = i * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    const uint4* q = p + (h % nslot) * 16;
+    uint4 v[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] = q[c];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc += v[c].x + v[c].y + v[c].z + v[c].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 // `hbm_read host BYTES`: the same reads over registered host memory (the
 // zero-copy and device-walk paths' source), through its device alias, beside
 // a hipMemcpy of the buffer to HBM: the PCIe ceiling the host-resident paths
@@ -259,6 +283,21 @@ static int host(uint64_t bytes) {
     report("slots_32B", g,
            time_it([&] { k_read_slots<<<g, 256>>>(p, nslot, reads, sink); }, 5),
            (double)reads * 32, (double)reads);
+  // the last column is lines per second here
+  const uint64_t lines = 2u << 20;
+  const int gl = (int)(lines / 256);
+  report("line_chunks_1", gl,
+         time_it([&] { k_read_line_chunks<1><<<gl, 256>>>(p, nslot, lines, sink); }, 5),
+         (double)lines * 128, (double)lines);
+  report("line_chunks_2", gl,
+         time_it([&] { k_read_line_chunks<2><<<gl, 256>>>(p, nslot, lines, sink); }, 5),
+         (double)lines * 128, (double)lines);
+  report("line_chunks_4", gl,
+         time_it([&] { k_read_line_chunks<4><<<gl, 256>>>(p, nslot, lines, sink); }, 5),
+         (double)lines * 128, (double)lines);
+  report("line_chunks_8", gl,
+         time_it([&] { k_read_line_chunks<8><<<gl, 256>>>(p, nslot, lines, sink); }, 5),
+         (double)lines * 128, (double)lines);
   printf("]}\n");
   CK(hipHostUnregister(h));
   free(h);
