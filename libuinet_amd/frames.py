@@ -339,3 +339,32 @@ def pkthdr_fields(ch: MbufChains):
     """(csum_flags, csum_data) of every packet's first mbuf."""
     first = ch.pkt_seg[:-1]
     return ch.mbufs["csum_flags"][first].copy(), ch.mbufs["csum_data"][first].copy()
+
+
+def split_headers(ch: MbufChains, seed: int, frac: float = 0.7, upto: int = 80) -> MbufChains:
+    """The same frames with the first mbuf of `frac` of them cut inside the
+    headers (at 1 .. `upto` bytes), sometimes with a zero-length mbuf after the
+    cut: the parse's reads that leave the first mbuf (offload_parse.h,
+    View::bytes / read) -- no generated batch splits a header otherwise."""
+    rng = np.random.default_rng(seed)
+    so, sl, ps = [], [], [0]
+    for i in range(ch.n):
+        a, e = int(ch.pkt_seg[i]), int(ch.pkt_seg[i + 1])
+        offs = [int(x) for x in ch.seg_off[a:e]]
+        lens = [int(x) for x in ch.seg_len[a:e]]
+        if lens and lens[0] > 1 and rng.random() < frac:
+            c = int(rng.integers(1, min(lens[0], upto)))
+            head = [(offs[0], c)] + ([(offs[0] + c, 0)] if rng.random() < 0.2 else [])
+            segs = head + [(offs[0] + c, lens[0] - c)] + list(zip(offs[1:], lens[1:]))
+        else:
+            segs = list(zip(offs, lens))
+        for o, ln in segs:
+            so.append(o)
+            sl.append(ln)
+        ps.append(len(so))
+    out = MbufChains(ch.arena, np.array(so, np.int64), np.array(sl, np.int64),
+                     np.array(ps, np.int64))
+    f_old, f_new = ch.pkt_seg[:-1], out.pkt_seg[:-1]
+    out.mbufs["csum_flags"][f_new] = ch.mbufs["csum_flags"][f_old]
+    out.mbufs["csum_data"][f_new] = ch.mbufs["csum_data"][f_old]
+    return out

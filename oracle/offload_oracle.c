@@ -39,7 +39,9 @@
  *                                         advertises CSUM_*_IPV6 must
  *
  * Chains whose link header reaches past the first mbuf are viewed through
- * a private copy of their mbuf headers (what m_adj would leave).
+ * a private copy of their mbuf headers (what m_adj would leave), and RX
+ * transport sums see the chain the way the stack's m_pullup calls leave it:
+ * headers contiguous in the first mbuf (pulled_up, below).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -141,6 +143,35 @@ chain_total(const struct oracle_mbuf *m)
 		if (m->m_len > 0)
 			t += m->m_len;
 	return t;
+}
+
+/*
+ * The chain as the transport's checksum sees it after the stack's pull-ups:
+ * ip_input.c:426,443 (the IP header), tcp_input.c:686 (IP header + TCP
+ * header), udp_usrreq.c:378 (+ UDP header), ip6_input.c:519 and
+ * IP6_EXTHDR_CHECK at tcp_input.c:535 / udp6_usrreq.c:200 (IPv6 header
+ * through the transport header) make the first `need` bytes contiguous before
+ * in_cksum_pseudo_header / in6_cksum read the headers from the first mbuf.
+ * When the first mbuf is shorter, the chain is viewed as one contiguous copy
+ * in `one` (m_pullup moves only the first `need` bytes; the sums do not see
+ * the difference); *buf is the caller's to free.
+ */
+static const struct oracle_mbuf *
+pulled_up(const struct oracle_mbuf *ipm, int need, struct oracle_mbuf *one, uint8_t **buf)
+{
+	long total;
+
+	*buf = NULL;
+	if (ipm->m_len >= need)
+		return ipm;
+	total = chain_total(ipm);
+	*buf = malloc(total > 0 ? (size_t)total : 1);
+	chain_bytes(ipm, 0, *buf, (int)total);
+	*one = *ipm;
+	one->m_next = NULL;
+	one->m_data = (char *)*buf;
+	one->m_len = (int)total;
+	return one;
 }
 
 /* Offset of the network header (l2len -1: Ethernet, optional 802.1Q), or -1;
@@ -251,7 +282,14 @@ rx6(struct oracle_mbuf *m, struct oracle_mbuf *ipm, const uint8_t *h, int got, l
 	} else if (nxt != 6) {
 		return st;
 	}
-	sum = oracle_in6_cksum(ipm, (uint8_t)nxt, (uint32_t)off, (uint32_t)tlen);
+	{
+		struct oracle_mbuf one;
+		uint8_t *buf;
+		const struct oracle_mbuf *p = pulled_up(ipm, off + (nxt == 6 ? 20 : 8), &one, &buf);
+
+		sum = oracle_in6_cksum(p, (uint8_t)nxt, (uint32_t)off, (uint32_t)tlen);
+		free(buf);
+	}
 	st |= S_RX_L4 | (sum == 0 ? S_RX_L4_OK : 0);
 	if (m->m_flags & O_M_PKTHDR) {
 		*csum_flags(m) |= O_CSUM_DATA_VALID | O_CSUM_PSEUDO_HDR;
@@ -309,8 +347,16 @@ oracle_rx_offload(struct oracle_mbuf *const *mv, int n, int l2len, uint8_t *stat
 		if (ip_len < hlen || chain_total(m) < (long)l3 + ip_len)
 			goto done;
 		if (proto == 6) {
-			sum = oracle_cksum_pseudo_header(ipm, ip_len - hlen, hlen, src, dst, 6);
+			struct oracle_mbuf one;
+			uint8_t *buf;
+			const struct oracle_mbuf *p = pulled_up(ipm, hlen + 20, &one, &buf);
+
+			sum = oracle_cksum_pseudo_header(p, ip_len - hlen, hlen, src, dst, 6);
+			free(buf);
 		} else if (proto == 17) {
+			struct oracle_mbuf one;
+			uint8_t *buf;
+			const struct oracle_mbuf *p;
 			int ulen;
 			if (got < hlen + 8)
 				goto done;
@@ -321,7 +367,9 @@ oracle_rx_offload(struct oracle_mbuf *const *mv, int n, int l2len, uint8_t *stat
 			ulen = h[hlen + 4] << 8 | h[hlen + 5];
 			if (ulen > ip_len - hlen || ulen < 8)
 				goto done;
-			sum = oracle_cksum_pseudo_header(ipm, ulen, hlen, src, dst, 17);
+			p = pulled_up(ipm, hlen + 8, &one, &buf);
+			sum = oracle_cksum_pseudo_header(p, ulen, hlen, src, dst, 17);
+			free(buf);
 		} else {
 			goto done;
 		}

@@ -214,6 +214,39 @@ def test_device_walk_hooks(ora, torch_dev):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("on_device", [True, False])
+def test_hooks_headers_split_across_mbufs(ora, torch_dev, on_device):
+    """RX and TX hooks on frames whose link / IP / L4 headers straddle the
+    first mbuf boundary (and zero-length mbufs), IPv4 with options and IPv6
+    with extension headers among them: on the device (mbufs registered, a
+    device-sized batch) and on the host hook, bit-exact against the oracle --
+    statuses, the sums written into the frames and the pkthdr marks."""
+    from libuinet_amd.frames import FrameBatch, pkthdr_fields, split_headers as resplit
+
+    n = 2600 if on_device else 1500
+    a = FrameBatch(n, seed=21, ipv6=0.3)
+    b = FrameBatch(n, seed=21, ipv6=0.3)
+    ta, tb = resplit(a.tx, 5), resplit(b.tx, 5)
+    regs = (a.arena, ta.mbufs) if on_device else ()
+    with registered(*regs):
+        st, nw = walks(lambda: u.tx_offload(ta.heads))
+    assert nw == (1 if on_device else 0)
+    assert np.array_equal(st, ora.tx_offload(tb.heads))
+    assert np.array_equal(a.arena, b.arena)
+    for x, y in zip(pkthdr_fields(ta), pkthdr_fields(tb)):
+        assert np.array_equal(x, y)
+    rx_a, arena_a, _ = a.rx(seed=6, corrupt=0.05)
+    rx_b, _, _ = b.rx(seed=6, corrupt=0.05)
+    ra, rb = resplit(rx_a, 7), resplit(rx_b, 7)
+    regs = (arena_a, ra.mbufs) if on_device else ()
+    with registered(*regs):
+        st, nw = walks(lambda: u.rx_offload(ra.heads))
+    assert nw == (1 if on_device else 0)
+    assert np.array_equal(st, ora.rx_offload(rb.heads))
+    for x, y in zip(pkthdr_fields(ra), pkthdr_fields(rb)):
+        assert np.array_equal(x, y)
+
+
 def test_device_hooks_fall_back_outside_regions(ora, torch_dev):
     """A TX batch one of whose frames has its first mbuf's data outside the
     registered regions: the device hook writes nothing and the host hook takes

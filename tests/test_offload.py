@@ -117,6 +117,33 @@ def test_rx_oracle_against_reference(frames, ora, ref):
     assert ((st[fb.kinds == "frag"] & RX_FRAG) != 0).all()
 
 
+def test_rx_oracle_header_splits_invariant(frames, ora):
+    """RX verdicts do not depend on where the first mbuf ends: the stack pulls
+    the headers up (ip_input.c:417-425 m_pullup, tcp_input.c:684-690) and the
+    sums run over the chain.  The oracle marks the same frames identically
+    with their headers cut across mbufs (and zero-length mbufs), IPv4 and IPv6
+    with extension headers -- the inputs tests/test_device_walk.py
+    ::test_hooks_headers_split_across_mbufs gives the engine."""
+    from libuinet_amd.frames import split_headers
+
+    fb = frames(seed=14, ipv6=0.3)
+    ora.tx_offload(fb.tx.heads)
+    rx, _, _ = fb.rx(seed=8, corrupt=0.1)
+    whole = ora.rx_offload(rx.heads)
+    f_whole = pkthdr_fields(rx)
+    split = split_headers(rx, 9)
+    assert split.n == rx.n and int(split.pkt_seg[-1]) > int(rx.pkt_seg[-1])
+    for x in pkthdr_fields(split):  # fresh marks
+        x[:] = 0
+    split.mbufs["csum_flags"][split.pkt_seg[:-1]] = 0
+    split.mbufs["csum_data"][split.pkt_seg[:-1]] = 0
+    rx.mbufs["csum_flags"][rx.pkt_seg[:-1]] = 0
+    rx.mbufs["csum_data"][rx.pkt_seg[:-1]] = 0
+    assert np.array_equal(ora.rx_offload(split.heads), whole)
+    for x, y in zip(pkthdr_fields(split), f_whole):
+        assert np.array_equal(x, y)
+
+
 # ---- IPv6 (ip6_output.c:188-209,966-981; tcp_input.c:627-639; udp6_usrreq.c:216-246)
 
 def _zoned(a: np.ndarray) -> bool:
