@@ -211,7 +211,7 @@ def test_fuzz_offload_hooks(ora):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from libuinet_amd.frames import FrameBatch, pkthdr_fields
+    from libuinet_amd.frames import FrameBatch, pkthdr_fields, split_headers
 
     frames = 0
     try:
@@ -231,27 +231,34 @@ def test_fuzz_offload_hooks(ora):
             b = FrameBatch(n, seed=seed, l2=l2, ipv6=ipv6)
             zc = bool(rng.integers(0, 2))
             mb = zc and bool(rng.integers(0, 2))  # mbufs registered: the GPU walks
+            # a third of the trials cut headers across the first mbuf boundary
+            sp = bool(rng.integers(0, 3) == 0)
+            ss = int(rng.integers(0, 2**31))
+            ta, tb = (split_headers(a.tx, ss), split_headers(b.tx, ss)) if sp else (a.tx, b.tx)
             if zc:
                 u.register_host(a.arena)
             if mb:
-                u.register_host(a.tx.mbufs)
+                u.register_host(ta.mbufs)
             try:
-                st_g = u.tx_offload(a.tx.heads, l2len)
+                st_g = u.tx_offload(ta.heads, l2len)
             finally:
                 if zc:
                     u.unregister_host(a.arena)
                 if mb:
-                    u.unregister_host(a.tx.mbufs)
-            st_o = ora.tx_offload(b.tx.heads, l2len)
-            ctx = f"offload trial {t}: n={n} l2={l2} ipv6={ipv6} zero_copy={zc} mbufs={mb}"
+                    u.unregister_host(ta.mbufs)
+            st_o = ora.tx_offload(tb.heads, l2len)
+            ctx = (f"offload trial {t}: n={n} l2={l2} ipv6={ipv6} zero_copy={zc} mbufs={mb} "
+                   f"split={sp}")
             assert np.array_equal(st_g, st_o), ctx + " (TX status)"
             assert np.array_equal(a.arena, b.arena), ctx + " (TX bytes)"
-            for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
+            for x, y in zip(pkthdr_fields(ta), pkthdr_fields(tb)):
                 assert np.array_equal(x, y), ctx + " (TX marks)"
             corrupt = float(rng.choice([0.0, 0.05, 0.5]))
             rs = int(rng.integers(0, 2**31))
             rx_a, arena_a, _ = a.rx(seed=rs, corrupt=corrupt)
             rx_b, _, _ = b.rx(seed=rs, corrupt=corrupt)
+            if sp:
+                rx_a, rx_b = split_headers(rx_a, ss + 1), split_headers(rx_b, ss + 1)
             if zc:
                 u.register_host(arena_a)
             if mb:
