@@ -525,7 +525,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   // 65535 B, else the 12-B wide ones.  The kernel reads them over PCIe, where a
   // byte costs ~140x what it does in HBM.  A group holding a longer piece is
   // written wide (its chunks flag it).
-#ifdef UINET_HOST_WIDE_DESC  // lab A/B build only (tools/r04_hostdesc.sh)
+#ifdef UINET_HOST_WIDE_DESC  // lab A/B build only (profiles/r04/scripts/r04_hostdesc.sh)
   const bool span32 = false;
 #else
   const bool span32 = hi_addr - lo_addr <= 0x100000000ull;
