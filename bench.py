@@ -528,6 +528,7 @@ def host_offload_line(keep, n: int, nbytes: int, gpu_out, ref_1t_s, reps: int = 
     rows.sort(key=lambda r: r[0])
     wall, st, out = rows[len(rows) // 2]
     k = n / 1000
+    link = link_h2d_gbs(keep["host"], bufs)
     return {
         "what": "the benchmarked batch as host mbufs in registered memory, through the host-mbuf "
                 "batch API (the GPU walks the chains over PCIe); median of %d calls" % reps,
@@ -538,7 +539,43 @@ def host_offload_line(keep, n: int, nbytes: int, gpu_out, ref_1t_s, reps: int = 
         "reference_1thread_ms": round(ref_1t_s * 1e3, 3) if ref_1t_s else None,
         "reference_1thread_cpu_us_per_1k_pkts": round(ref_1t_s * 1e6 / k, 3) if ref_1t_s else None,
         "bit_identical": bool(all(np.array_equal(r[2], gpu_out) for r in rows)),
+        # the link's own rate, measured here: one DMA copy of the same registered
+        # bytes to HBM; the batch's summed bytes over its wall time against it
+        # (the walk's mbuf lines also cross the link and are not counted above)
+        "link_h2d_gbs": link,
+        "frac_of_link": round(nbytes / wall / 1e9 / link, 4) if link else None,
     }
+
+
+def link_h2d_gbs(host, bufs):
+    """GB/s of a DMA copy of `host` (registered again for the copy) into HBM,
+    best of 3; None if it cannot be measured."""
+    import torch
+
+    import libuinet_amd as u
+
+    try:
+        for b in bufs:
+            u.register_host(b)
+        try:
+            h = torch.from_numpy(host)
+            d = torch.empty(h.shape, dtype=h.dtype, device="cuda")
+            d.copy_(h)
+            torch.cuda.synchronize()
+            best = None
+            for _ in range(3):
+                t0 = time.perf_counter()
+                d.copy_(h)
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            del d
+            return round(host.nbytes / best / 1e9, 2)
+        finally:
+            for b in bufs:
+                u.unregister_host(b)
+    except Exception:  # a report, never the measurement
+        return None
 
 
 def main():

@@ -115,3 +115,6 @@ def test_bench_n1_host_resident_cpu_line(torch_dev):
     assert h["bit_identical"] is True and h["device_walked"] is True
     assert h["wall_ms"] > 0 and h["host_cpu_us_per_1k_pkts"] > 0
     assert h["reference_1thread_cpu_us_per_1k_pkts"] > 0
+    # the link's own DMA rate, measured in the same run, and the batch against it
+    assert h["link_h2d_gbs"] and h["link_h2d_gbs"] > 1.0
+    assert 0 < h["frac_of_link"] < 1.5
