@@ -170,3 +170,23 @@ def test_per_call_edge_lengths(ora, length):
         for skip in (0, 1, min(length, 20)):
             want = ora.skip_batch(ch.heads, length, skip)[0]
             assert u.in_cksum_skip(ch.head(0), length, skip) == want, (off, skip)
+
+
+def test_per_call_simd_edges(ora):
+    """Piece lengths around the vector folds' thresholds and steps (AVX2 from
+    128 B in 64-B steps, AVX-512 from 256 B in 128-B steps, cksum_percall.cpp)
+    at every start offset within a 64-B line, whole and cut by skip, against
+    the oracle: the scalar tail after a vector run keeps each byte's weight."""
+    arena = aligned_empty(1 << 16)
+    splitmix64_bytes(arena.size, 99, out=arena)
+    lengths = [127, 128, 129, 191, 192, 255, 256, 257, 383, 384, 385, 511, 512, 513, 1023, 4097]
+    offs, lens = [], []
+    for ln in lengths:
+        for off in range(64):
+            offs.append(64 * len(offs) % 40000 + off)
+            lens.append(ln)
+    ch = MbufChains(arena, offs, lens, np.arange(len(offs) + 1))
+    for skip in (0, 1, 3):
+        want = ora.skip_batch(ch.heads, np.array(lens), skip)
+        got = np.array([u.in_cksum_skip(ch.head(i), lens[i], skip) for i in range(ch.n)])
+        np.testing.assert_array_equal(got, want)
