@@ -119,7 +119,7 @@ def test_rx_oracle_against_reference(frames, ora, ref):
 
 def test_rx_oracle_header_splits_invariant(frames, ora):
     """RX verdicts do not depend on where the first mbuf ends: the stack pulls
-    the headers up (ip_input.c:417-425 m_pullup, tcp_input.c:684-690) and the
+    the headers up (ip_input.c:426,443 m_pullup, tcp_input.c:686) and the
     sums run over the chain.  The oracle marks the same frames identically
     with their headers cut across mbufs (and zero-length mbufs), IPv4 and IPv6
     with extension headers -- the inputs tests/test_device_walk.py
@@ -386,6 +386,72 @@ def test_pcap_rx_offload_gpu(torch_dev, ora, pcap_frames):
     rx_g, _ = _pcap_rx(pcap_frames)
     rx_o, _ = _pcap_rx(pcap_frames)
     np.testing.assert_array_equal(u.rx_offload(rx_g.heads), ora.rx_offload(rx_o.heads))
+    for x, y in zip(pkthdr_fields(rx_g), pkthdr_fields(rx_o)):
+        np.testing.assert_array_equal(x, y)
+
+
+def _pcap_fragmented(frames, seed):
+    """The capture's frames re-chained as m_fragment() does under
+    MBUF_STRESS_TEST (uipc_mbuf.c:1693-1761): random 1-256-B mbufs, each at a
+    random 0-7-B offset (SURVEY.md section 4's KAT)."""
+    from libuinet_amd.mbuf import MbufChains, aligned_empty
+
+    rng = np.random.default_rng(seed)
+    arena = aligned_empty(sum(len(f) for f in frames) * 2 + 8 * 4096)
+    seg_off, seg_len, pkt_seg, cur = [], [], [0], 0
+    for f in frames:
+        b = np.frombuffer(f, np.uint8)
+        i = 0
+        while i < b.size:
+            k = min(int(rng.integers(1, 257)), b.size - i)
+            cur += int(rng.integers(0, 8))
+            arena[cur:cur + k] = b[i:i + k]
+            seg_off.append(cur)
+            seg_len.append(k)
+            cur += k
+            i += k
+        pkt_seg.append(len(seg_off))
+    return MbufChains(arena, seg_off, seg_len, pkt_seg), arena
+
+
+def test_pcap_rx_offload_fragmented_oracle(ora, pcap_frames):
+    """the capture verifies to 0 also when every frame
+    is re-chained into random 1-256-B fragments -- through the RX hook's
+    restatement (the stack's pull-ups modelled) every TCP frame is still
+    marked IP-valid and data-valid, exactly as unfragmented."""
+    for seed in (1, 2, 3):
+        rx, _ = _pcap_fragmented(pcap_frames, seed)
+        st = ora.rx_offload(rx.heads)
+        tcp = (st & RX_L4) != 0
+        assert tcp.sum() >= 113
+        assert ((st[tcp] & (RX_IPV4 | RX_IP_OK | RX_L4 | RX_L4_OK)) == 0x0F).all()
+        _, cd = pkthdr_fields(rx)
+        assert (cd[tcp] == 0xFFFF).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("registered", [False, True])
+def test_pcap_rx_offload_fragmented_gpu(torch_dev, ora, pcap_frames, registered):
+    """The same fragmented capture through the engine's RX hook: the host hook
+    (staged), and with mbufs and bytes registered the device hook (the capture
+    repeated 20 times, 2,260 frames: a device-sized batch), against the oracle."""
+    import libuinet_amd as u
+
+    frames = list(pcap_frames) * (20 if registered else 1)
+    rx_g, arena_g = _pcap_fragmented(frames, 4)
+    rx_o, _ = _pcap_fragmented(frames, 4)
+    regs = (arena_g, rx_g.mbufs) if registered else ()
+    for b in regs:
+        u.register_host(b)
+    try:
+        before = u.host_cpu()["device_walks"]
+        st = u.rx_offload(rx_g.heads)
+        walked = u.host_cpu()["device_walks"] - before
+    finally:
+        for b in regs:
+            u.unregister_host(b)
+    assert walked == (1 if registered else 0)
+    np.testing.assert_array_equal(st, ora.rx_offload(rx_o.heads))
     for x, y in zip(pkthdr_fields(rx_g), pkthdr_fields(rx_o)):
         np.testing.assert_array_equal(x, y)
 

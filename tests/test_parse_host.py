@@ -169,3 +169,24 @@ def test_host_parse_matches_oracle_hooks(parse_lib, ora, seed, ipv6, l2, cut):
     for x, y in zip(pkthdr_fields(rx_a), pkthdr_fields(rx_b)):
         assert np.array_equal(x, y)
     assert (want & RX_L4).any() and (want & RX_L4_OK).any()  # the sums did run
+
+
+def test_host_parse_fragmented_capture(parse_lib, ora, pcap_frames):
+    """The reference's capture re-chained into random 1-256-B fragments
+    (SURVEY.md section 4's KAT): the shared parse's jobs, folded by the oracle,
+    verify every TCP frame to 0 -- the same marks as the oracle's RX hook."""
+    from test_offload import _pcap_fragmented
+
+    for seed in (5, 6):
+        rx, _ = _pcap_fragmented(pcap_frames, seed)
+        rx_b, _ = _pcap_fragmented(pcap_frames, seed)
+        n = rx.n
+        jm, jl, js, jd = _jobs(n)
+        ip_job, l4_job, st = (np.zeros(n, np.uint8) for _ in range(3))
+        heads = np.ascontiguousarray(rx.heads, np.uint64)
+        parse_lib.parse_rx(_ptr(heads), n, -1, _ptr(jm), _ptr(jl), _ptr(js), _ptr(jd),
+                           _ptr(ip_job), _ptr(l4_job), _ptr(st))
+        st = _rx_apply(rx, st, ip_job, l4_job, _results(ora, jm, jl, js, jd))
+        want = ora.rx_offload(rx_b.heads)
+        assert np.array_equal(st, want)
+        assert ((want & 0x0F) == 0x0F).sum() >= 113
