@@ -137,8 +137,12 @@ __attribute__((target("avx512f"))) uint64_t piece_sum_avx512(const uint8_t* p, s
 #ifndef UINET_LAB_SIMD_MAX
 #define UINET_LAB_SIMD_MAX 2
 #endif
-const int g_simd = std::min(UINET_LAB_SIMD_MAX, __builtin_cpu_supports("avx512f") ? 2
-                                                : __builtin_cpu_supports("avx2") ? 1 : 0);
+// (a static initializer may run before libgcc's own CPU detection: run it)
+const int g_simd = [] {
+  __builtin_cpu_init();
+  return std::min(UINET_LAB_SIMD_MAX, __builtin_cpu_supports("avx512f") ? 2
+                                      : __builtin_cpu_supports("avx2") ? 1 : 0);
+}();
 
 inline uint64_t piece_sum_best(const uint8_t* p, size_t n) {
   if (n >= 256 && g_simd == 2) return piece_sum_avx512(p, n);
