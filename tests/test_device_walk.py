@@ -247,6 +247,53 @@ def test_hooks_headers_split_across_mbufs(ora, torch_dev, on_device):
         assert np.array_equal(x, y)
 
 
+def _payload_outside(ch, arena, k, other):
+    """Point frame k's second mbuf at a copy of its bytes in `other` (outside
+    the registered regions); returns the copy's offset in `other`."""
+    seg = int(ch.pkt_seg[k]) + 1
+    ln = int(ch.mbufs["m_len"][seg])
+    src = int(ch.mbufs["m_data"][seg]) - arena.ctypes.data
+    other[:ln] = arena[src:src + ln]
+    ch.mbufs["m_data"][seg] = other.ctypes.data
+
+
+def test_device_hooks_walk_flag_in_last_group(ora, torch_dev):
+    """Batches of 20,000 frames (the device hook walks them in several groups
+    on two streams): one frame in the last group has a payload mbuf outside the
+    registered regions.  The parse, which reads only the first mbuf, takes it;
+    the walk flags it, so the apply writes nothing in any group and the host
+    hook takes the whole batch -- equal to the oracle, TX and RX.  (Writing
+    the other groups on the device and redoing only the flagged one measured
+    no faster: profiles/r05/pruned/hook_apply_per_group.diff.)"""
+    from libuinet_amd.frames import FrameBatch, pkthdr_fields
+
+    n = 20000
+    a = FrameBatch(n, seed=41)
+    b = FrameBatch(n, seed=41)
+    k = int(np.flatnonzero(np.diff(a.tx.pkt_seg) >= 2)[-1])  # a chained frame near the end
+    oa, ob = rand_arena(1 << 16, 3), rand_arena(1 << 16, 3)
+    _payload_outside(a.tx, a.arena, k, oa)
+    _payload_outside(b.tx, b.arena, k, ob)
+    with registered(a.arena, a.tx.mbufs):
+        st, nw = walks(lambda: u.tx_offload(a.tx.heads))
+    assert nw == 0  # the host hook took the batch
+    assert np.array_equal(st, ora.tx_offload(b.tx.heads))
+    assert np.array_equal(a.arena, b.arena)
+    for x, y in zip(pkthdr_fields(a.tx), pkthdr_fields(b.tx)):
+        assert np.array_equal(x, y)
+    rx_a, arena_a, _ = a.rx(seed=42, corrupt=0.05)
+    rx_b, arena_b, _ = b.rx(seed=42, corrupt=0.05)
+    k = int(np.flatnonzero(np.diff(rx_a.pkt_seg) >= 2)[-1])
+    _payload_outside(rx_a, arena_a, k, oa)
+    _payload_outside(rx_b, arena_b, k, ob)
+    with registered(arena_a, rx_a.mbufs):
+        st, nw = walks(lambda: u.rx_offload(rx_a.heads))
+    assert nw == 0
+    assert np.array_equal(st, ora.rx_offload(rx_b.heads))
+    for x, y in zip(pkthdr_fields(rx_a), pkthdr_fields(rx_b)):
+        assert np.array_equal(x, y)
+
+
 def test_device_hooks_fall_back_outside_regions(ora, torch_dev):
     """A TX batch one of whose frames has its first mbuf's data outside the
     registered regions: the device hook writes nothing and the host hook takes
