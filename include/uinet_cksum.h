@@ -335,7 +335,8 @@ int uinet_cksum_rx_offload(struct mbuf *const *m, int n, int l2len,
 #define UINET_TX_L4      0x01 /* th_sum / uh_sum computed and stored */
 #define UINET_TX_IP      0x02 /* ip_sum computed and stored */
 #define UINET_TX_L4_LOST 0x04 /* checksum field beyond the first mbuf: not stored */
-#define UINET_TX_SKIP    0x08 /* no M_PKTHDR, not IP, nothing asked, or CSUM_TSO */
+#define UINET_TX_SKIP    0x08 /* no M_PKTHDR, not IP, nothing asked, CSUM_TSO, or an
+                                 IP header the chain cuts short */
 #define UINET_TX_IPV6    0x10 /* an IPv6 packet (with UINET_TX_L4 or _L4_LOST) */
 
 /* TX (if_netmap_batch_send, uinet_if_netmap.c:1196-1262, with if_hwassist =

@@ -368,3 +368,82 @@ def split_headers(ch: MbufChains, seed: int, frac: float = 0.7, upto: int = 80) 
     out.mbufs["csum_flags"][f_new] = ch.mbufs["csum_flags"][f_old]
     out.mbufs["csum_data"][f_new] = ch.mbufs["csum_data"][f_old]
     return out
+
+
+def mangle_headers(ch: MbufChains, fb: FrameBatch, seed: int, frac: float = 0.5) -> MbufChains:
+    """The same frames with `frac` of them made malformed the ways the stack's
+    input checks name (ip_input.c:416-500, ip6_input.c:519-700, udp_usrreq.c:
+    404-420, udp6_usrreq.c:216-230): a wrong version or header length nibble,
+    a wrong ethertype, IP / IPv6 / UDP length fields too short or too long, a
+    transport or extension-header type or length changed, the chain cut
+    inside its headers, or nothing but empty mbufs.  Header bytes are changed
+    in `ch`'s arena in place (apply the same seed to a twin batch for the
+    oracle); the returned chains carry the cuts.  `fb` is the batch the frames
+    came from (its l3 / header offsets)."""
+    rng = np.random.default_rng(seed)
+    so, sl, ps = [], [], [0]
+    for i in range(ch.n):
+        a, e = int(ch.pkt_seg[i]), int(ch.pkt_seg[i + 1])
+        offs = [int(x) for x in ch.seg_off[a:e]]
+        lens = [int(x) for x in ch.seg_len[a:e]]
+        size = sum(lens)
+
+        def poke(j, v):
+            for o, ln in zip(offs, lens):
+                if j < ln:
+                    ch.arena[o + j] = v & 0xFF
+                    return
+                j -= ln
+
+        def peek(j):
+            for o, ln in zip(offs, lens):
+                if j < ln:
+                    return int(ch.arena[o + j])
+                j -= ln
+            return 0
+
+        l3, hl, v6 = int(fb.l3[i]), int(fb.hlen[i]), bool(fb.v6[i])
+        kind = int(rng.integers(0, 9)) if size > l3 and rng.random() < frac else -1
+        if kind == 0:  # header length nibble
+            poke(l3, (peek(l3) & 0xF0) | int(rng.integers(0, 16)))
+        elif kind == 1:  # version nibble
+            poke(l3, int(rng.integers(0, 16)) << 4 | (peek(l3) & 0x0F))
+        elif kind == 2 and l3 >= 14:  # ethertype
+            t = [(0x08, 0x00), (0x86, 0xDD), (0x81, 0x00), (0x08, 0x06),
+                 tuple(int(x) for x in rng.integers(0, 256, 2))][int(rng.integers(0, 5))]
+            poke(l3 - 2, t[0])
+            poke(l3 - 1, t[1])
+        elif kind == 3:  # IP total / IPv6 payload length
+            act = size - l3 - (40 if v6 else 0)
+            v = int(rng.choice([0, 1, 7, max(hl - 1, 0), hl, act - 1, act + 1, 65535,
+                                int(rng.integers(0, 65536))])) & 0xFFFF
+            poke(l3 + (4 if v6 else 2), v >> 8)
+            poke(l3 + (5 if v6 else 3), v)
+        elif kind == 4 and fb.kinds[i] in ("udp", "udp0"):  # UDP length
+            act = size - l3 - hl
+            v = int(rng.choice([0, 7, 8, act - 1, act + 1, 65535])) & 0xFFFF
+            poke(l3 + hl + 4, v >> 8)
+            poke(l3 + hl + 5, v)
+        elif kind == 5:  # the chain cut inside or just past its headers
+            keep = int(rng.integers(0, min(size, l3 + hl + 28) + 1))
+            nl = []
+            for ln in lens:
+                nl.append(min(ln, keep))
+                keep -= nl[-1]
+            lens = nl
+        elif kind == 6 and v6:  # the first extension header's length
+            poke(l3 + 41, int(rng.integers(0, 256)))
+        elif kind == 7:  # only empty mbufs
+            lens = [0] * len(lens)
+        elif kind == 8:  # transport / next-header type
+            pool = [0, 6, 17, 43, 44, 58, 59, 60] if v6 else [0, 1, 6, 17, 44, 58]
+            poke(l3 + (6 if v6 else 9), int(rng.choice(pool + [int(rng.integers(0, 256))])))
+        so.extend(offs)
+        sl.extend(lens)
+        ps.append(len(so))
+    out = MbufChains(ch.arena, np.array(so, np.int64), np.array(sl, np.int64),
+                     np.array(ps, np.int64))
+    f_old, f_new = ch.pkt_seg[:-1], out.pkt_seg[:-1]
+    out.mbufs["csum_flags"][f_new] = ch.mbufs["csum_flags"][f_old]
+    out.mbufs["csum_data"][f_new] = ch.mbufs["csum_data"][f_old]
+    return out

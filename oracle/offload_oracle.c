@@ -432,7 +432,10 @@ oracle_tx_offload(struct oracle_mbuf *const *mv, int n, int l2len, uint8_t *stat
 		}
 		if ((fl & O_CSUM_TSO) || !(fl & (O_CSUM_IP | O_CSUM_TCP | O_CSUM_UDP)) ||
 		    ver != 4 || chain_bytes(m, l3, h, 20) < 20 ||
-		    (h[0] >> 4) != 4 || (hlen = (h[0] & 15) << 2) < 20) {
+		    (h[0] >> 4) != 4 || (hlen = (h[0] & 15) << 2) < 20 ||
+		    chain_total(m) - l3 < hlen) {
+			/* a header the chain cuts short is left alone (the stack
+			 * never builds one; in_cksum would sum what is there) */
 			st = S_TX_SKIP;
 			goto done;
 		}

@@ -247,6 +247,47 @@ def test_hooks_headers_split_across_mbufs(ora, torch_dev, on_device):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("mode", ["device", "bytes", "host"])
+def test_hooks_malformed_frames(ora, torch_dev, mode):
+    """RX and TX hooks on batches where most frames are malformed the ways the
+    stack's input checks name (frames.mangle_headers: version / header-length
+    nibbles, ethertype, IP / IPv6 / UDP lengths, next-header types, extension
+    lengths, chains cut inside their headers, only empty mbufs), headers also
+    cut across mbufs: on the device hook (mbufs and frames registered), the
+    host hook over registered frames, and the staged host hook -- statuses,
+    stored sums and marks bit-exact against the oracle."""
+    from libuinet_amd.frames import FrameBatch, mangle_headers, pkthdr_fields, split_headers
+
+    n = 2600 if mode == "device" else 1500
+    for l2, seed in ((True, 41), (False, 42)):
+        l2len = -1 if l2 else 0
+        a = FrameBatch(n, seed=seed, l2=l2, ipv6=0.4)
+        b = FrameBatch(n, seed=seed, l2=l2, ipv6=0.4)
+        ta, tb = mangle_headers(a.tx, a, seed, 0.7), mangle_headers(b.tx, b, seed, 0.7)
+        ta, tb = split_headers(ta, seed + 1, 0.3), split_headers(tb, seed + 1, 0.3)
+        regs = {"device": (a.arena, ta.mbufs), "bytes": (a.arena,), "host": ()}[mode]
+        with registered(*regs):
+            st, nw = walks(lambda: u.tx_offload(ta.heads, l2len))
+        assert nw == (1 if mode == "device" else 0)
+        assert np.array_equal(st, ora.tx_offload(tb.heads, l2len)), (l2, "TX")
+        assert np.array_equal(a.arena, b.arena)
+        for x, y in zip(pkthdr_fields(ta), pkthdr_fields(tb)):
+            assert np.array_equal(x, y)
+        rx_a, arena_a, _ = a.rx(seed=seed + 2, corrupt=0.05)
+        rx_b, _, _ = b.rx(seed=seed + 2, corrupt=0.05)
+        ra, rb = mangle_headers(rx_a, a, seed + 3, 0.7), mangle_headers(rx_b, b, seed + 3, 0.7)
+        ra, rb = split_headers(ra, seed + 4, 0.3), split_headers(rb, seed + 4, 0.3)
+        regs = {"device": (arena_a, ra.mbufs), "bytes": (arena_a,), "host": ()}[mode]
+        with registered(*regs):
+            st, nw = walks(lambda: u.rx_offload(ra.heads, l2len))
+        assert nw == (1 if mode == "device" else 0)
+        want = ora.rx_offload(rb.heads, l2len)
+        assert np.array_equal(st, want), (l2, "RX", np.flatnonzero(st != want)[:8])
+        for x, y in zip(pkthdr_fields(ra), pkthdr_fields(rb)):
+            assert np.array_equal(x, y)
+        assert (want & 0x08).any() and (want == 0).any()  # verified frames and unmarked ones
+
+
 def _payload_outside(ch, arena, k, other):
     """Point frame k's second mbuf at a copy of its bytes in `other` (outside
     the registered regions); returns the copy's offset in `other`."""

@@ -27,6 +27,7 @@ KNOBS = {"blocks_per_cu": [0, 0, 1, 3, 64], "chains_pass": [2, 2, 4], "chains_lo
 HINTS = (0, 64, 80, 200, 500, 1500, 4000, 9000)
 ARENA = 8 << 20
 TRIALS = int(os.environ.get("UINET_FUZZ_TRIALS", "300"))  # longer hunts: set it
+BASE = int(os.environ.get("UINET_FUZZ_BASE", "0"))  # and this, for seeds not yet run
 
 
 def _lengths(rng, n):
@@ -39,7 +40,7 @@ def _lengths(rng, n):
 
 
 def _trial(torch, ora, arena, d_arena, t):
-    rng = np.random.default_rng(90000 + t)
+    rng = np.random.default_rng(90000 + BASE + t)
     knobs = {k: int(rng.choice(vals)) for k, vals in KNOBS.items()}
     for k, v in knobs.items():
         u.set_tuning(k, v)
@@ -134,7 +135,7 @@ HOST_DEFAULTS = {"host_threads": min(16, os.cpu_count() or 1), "walk_prefetch": 
 def _host_trial(ora, arena, t):
     from libuinet_amd.mbuf import MbufChains
 
-    rng = np.random.default_rng(70000 + t)
+    rng = np.random.default_rng(70000 + BASE + t)
     u.set_tuning("host_threads", int(rng.choice([1, 2, 5, 16])))
     u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
     u.set_tuning("host_pin", int(rng.integers(0, 2)))
@@ -211,12 +212,12 @@ def test_fuzz_offload_hooks(ora):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from libuinet_amd.frames import FrameBatch, pkthdr_fields, split_headers
+    from libuinet_amd.frames import FrameBatch, mangle_headers, pkthdr_fields, split_headers
 
     frames = 0
     try:
         for t in range(max(1, TRIALS // 10)):
-            rng = np.random.default_rng(50000 + t)
+            rng = np.random.default_rng(50000 + BASE + t)
             u.set_tuning("host_threads", int(rng.choice([1, 3, 16])))
             u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
             u.set_tuning("walk_device", int(rng.integers(0, 2)))
@@ -234,7 +235,10 @@ def test_fuzz_offload_hooks(ora):
             # a third of the trials cut headers across the first mbuf boundary
             sp = bool(rng.integers(0, 3) == 0)
             ss = int(rng.integers(0, 2**31))
-            ta, tb = (split_headers(a.tx, ss), split_headers(b.tx, ss)) if sp else (a.tx, b.tx)
+            # a quarter make half their frames malformed (frames.mangle_headers)
+            mg = float(rng.choice([0.0, 0.0, 0.0, 0.5]))
+            ta, tb = (mangle_headers(a.tx, a, ss, mg), mangle_headers(b.tx, b, ss, mg)) if mg else (a.tx, b.tx)
+            ta, tb = (split_headers(ta, ss), split_headers(tb, ss)) if sp else (ta, tb)
             if zc:
                 u.register_host(a.arena)
             if mb:
@@ -248,7 +252,7 @@ def test_fuzz_offload_hooks(ora):
                     u.unregister_host(ta.mbufs)
             st_o = ora.tx_offload(tb.heads, l2len)
             ctx = (f"offload trial {t}: n={n} l2={l2} ipv6={ipv6} zero_copy={zc} mbufs={mb} "
-                   f"split={sp}")
+                   f"split={sp} malformed={mg}")
             assert np.array_equal(st_g, st_o), ctx + " (TX status)"
             assert np.array_equal(a.arena, b.arena), ctx + " (TX bytes)"
             for x, y in zip(pkthdr_fields(ta), pkthdr_fields(tb)):
@@ -257,6 +261,8 @@ def test_fuzz_offload_hooks(ora):
             rs = int(rng.integers(0, 2**31))
             rx_a, arena_a, _ = a.rx(seed=rs, corrupt=corrupt)
             rx_b, _, _ = b.rx(seed=rs, corrupt=corrupt)
+            if mg:
+                rx_a, rx_b = mangle_headers(rx_a, a, ss + 2, mg), mangle_headers(rx_b, b, ss + 2, mg)
             if sp:
                 rx_a, rx_b = split_headers(rx_a, ss + 1), split_headers(rx_b, ss + 1)
             if zc:

@@ -17,7 +17,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from libuinet_amd.frames import FrameBatch, pkthdr_fields, split_headers
+from libuinet_amd.frames import FrameBatch, mangle_headers, pkthdr_fields, split_headers
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -124,18 +124,21 @@ def _tx_apply(ch, arena, st, ip_job, l4_job, udp, l4_store, ip_l3, clear, res):
     return st
 
 
-CASES = [  # (seed, ipv6 share, link header, cut headers across mbufs)
-    (31, 0.0, True, False), (32, 0.3, True, False), (33, 1.0, False, False),
-    (34, 0.3, True, True), (35, 0.5, False, True)]
+CASES = [  # (seed, ipv6 share, link header, cut headers across mbufs, malformed share)
+    (31, 0.0, True, False, 0.0), (32, 0.3, True, False, 0.0), (33, 1.0, False, False, 0.0),
+    (34, 0.3, True, True, 0.0), (35, 0.5, False, True, 0.0),
+    (36, 0.0, True, False, 0.6), (37, 0.5, True, True, 0.6), (38, 1.0, False, True, 0.6)]
 
 
-@pytest.mark.parametrize("seed,ipv6,l2,cut", CASES)
-def test_host_parse_matches_oracle_hooks(parse_lib, ora, seed, ipv6, l2, cut):
+@pytest.mark.parametrize("seed,ipv6,l2,cut,bad", CASES)
+def test_host_parse_matches_oracle_hooks(parse_lib, ora, seed, ipv6, l2, cut, bad):
     n = 1200
     l2len = -1 if l2 else 0
     a = FrameBatch(n, seed=seed, l2=l2, ipv6=ipv6)
     b = FrameBatch(n, seed=seed, l2=l2, ipv6=ipv6)
     ta, tb = (split_headers(a.tx, seed), split_headers(b.tx, seed)) if cut else (a.tx, b.tx)
+    if bad:  # malformed headers, cut chains, empty mbufs (frames.mangle_headers)
+        ta, tb = mangle_headers(ta, a, seed + 3, bad), mangle_headers(tb, b, seed + 3, bad)
 
     # TX
     jm, jl, js, jd = _jobs(n)
@@ -155,6 +158,8 @@ def test_host_parse_matches_oracle_hooks(parse_lib, ora, seed, ipv6, l2, cut):
     # RX over the transmitted frames, some corrupted
     rx_a, _, _ = a.rx(seed=seed + 1, corrupt=0.1)
     rx_b, _, _ = b.rx(seed=seed + 1, corrupt=0.1)
+    if bad:
+        rx_a, rx_b = mangle_headers(rx_a, a, seed + 4, bad), mangle_headers(rx_b, b, seed + 4, bad)
     if cut:
         rx_a, rx_b = split_headers(rx_a, seed + 2), split_headers(rx_b, seed + 2)
     jm, jl, js, jd = _jobs(n)
