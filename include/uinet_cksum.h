@@ -171,13 +171,17 @@ int uinet_cksum_device_ok(void);
  *   "walk_device"     host-mbuf batches (2c, 2d) whose mbufs AND bytes lie in
  *                     registered memory: 1 (default) the GPU walks the chains,
  *                     the host only writes the jobs; 0 the host walks them
+ *   "chains_wide"     chain API: 0 (default) one wave per packet when
+ *                     len_hint (mean segment bytes) is >= 2048, else the
+ *                     tile kernel; 1 = always the tile kernel, 2 = always
+ *                     one wave per packet
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU,
  * UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG, UINET_CKSUM_CHAINS_TILE,
  * UINET_CKSUM_XCD_REMAP, UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF,
  * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_PIPE, UINET_CKSUM_HOST_PIN,
- * UINET_CKSUM_MULTI_GATHER and UINET_CKSUM_WALK_DEVICE set the initial
- * values. */
+ * UINET_CKSUM_MULTI_GATHER, UINET_CKSUM_WALK_DEVICE and
+ * UINET_CKSUM_CHAINS_WIDE set the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
 /* ------------------------------------------------------------------------ */

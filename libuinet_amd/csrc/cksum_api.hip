@@ -66,7 +66,7 @@ void note_kernel(const void* host_stub) { t_last_kernel = host_stub; }
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, chains_pass{2}, host_threads{8}, chains_long{128},
       chains_tile{0}, xcd_remap{1}, walk_prefetch{1}, spans_geo{0}, spans_pipe{1},
-      host_pin{0}, multi_gather{0}, walk_device{1};
+      host_pin{0}, multi_gather{0}, walk_device{1}, chains_wide{0};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -90,6 +90,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
       {"walk_device", &TuningLive::walk_device, [](int v) { return v == 0 || v == 1; }},
+      {"chains_wide", &TuningLive::chains_wide, [](int v) { return v >= 0 && v <= 2; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -108,7 +109,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_GEO", "spans_geo"},
         {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},
         {"UINET_CKSUM_HOST_PIN", "host_pin"},          {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},
-        {"UINET_CKSUM_WALK_DEVICE", "walk_device"},
+        {"UINET_CKSUM_WALK_DEVICE", "walk_device"},     {"UINET_CKSUM_CHAINS_WIDE", "chains_wide"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -139,6 +140,7 @@ Tuning tuning() {
   x.host_pin = ld(t.host_pin);
   x.multi_gather = ld(t.multi_gather);
   x.walk_device = ld(t.walk_device);
+  x.chains_wide = ld(t.chains_wide);
   return x;
 }
 

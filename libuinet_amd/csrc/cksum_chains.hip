@@ -52,6 +52,7 @@ typedef unsigned short us16x2 __attribute__((ext_vector_type(2)));
 #endif
 constexpr int kLongU = UINET_CHAINS_LONGU;  // chunks in flight per lane on a long segment
 constexpr uint32_t kListMax = 1024;  // longest segment (chunks) the chunk list takes
+constexpr uint32_t kWideHint = 2048;  // mean segment bytes from which k_chains_wide runs
 
 // 16-B raw buffer load, non-temporal (aux bit 1), from a resource spanning
 // 4 GiB: one VGPR of offset instead of a 64-bit address per chunk.
@@ -399,15 +400,98 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
 }
 
 
+// k_chains_wide: one wave per packet, for chains of few long segments (a TSO
+// engine's 40-B header mbuf + 9 KB payload slice, config 5tso).  The tile
+// kernel above streams such a segment with 2 chunks per lane in flight (its
+// 72-VGPR budget) and serialises a tile's 32 packets in one wave; here every
+// packet is a wave of its own and each segment goes out as kWideU chunks per
+// lane at once -- the span kernel's 64 x 9 shape, 9 KiB per load round.  The
+// segments of a packet are walked in order with wave-uniform (scalar)
+// descriptor reads, clipped to [skip, len) exactly as describe_round does,
+// summed into (even, odd) logical-parity accumulators, and the odd one is
+// byte-rotated once at the end (in_cksum.c:222-225).
+constexpr int kWideU = 9;
+template <typename OffT, typename LenT>
+__global__ __launch_bounds__(kBlock) void k_chains_wide(const uint8_t* __restrict__ base,
+                                                       const OffT* __restrict__ seg_off,
+                                                       const LenT* __restrict__ seg_len,
+                                                       const uint32_t* __restrict__ pkt_seg,
+                                                       const uint32_t* __restrict__ plen,
+                                                       const uint32_t* __restrict__ pskip,
+                                                       const uint32_t* __restrict__ seed,
+                                                       uint16_t* __restrict__ out, uint32_t n,
+                                                       uint32_t flags) {
+  __shared__ MaskLut lut;
+  lut.init();
+  const int lane = threadIdx.x & 63;
+  const uint32_t wstride = gridDim.x * kWaves;
+  for (uint32_t p = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+       p < n; p += wstride) {
+    const uint32_t S0 = pkt_seg[p], S1 = pkt_seg[p + 1];
+    const uint32_t sk = pskip ? pskip[p] : 0u;
+    const uint32_t ln = plen ? plen[p] : 0xffffffffu;
+    uint64_t ev = 0, od = 0;  // this lane's chunk sums by logical parity
+    uint32_t pos = 0;         // chain offset of segment s
+    for (uint32_t s = S0; s < S1; ++s) {
+      const uint32_t l = (uint32_t)seg_len[s];
+      const uint32_t lo = sk > pos ? min(sk - pos, l) : 0u;
+      const uint32_t hi = ln > pos ? min(ln - pos, l) : 0u;
+      if (hi > lo) {
+        const uint32_t eff = hi - lo;
+        const uint8_t* a = base + (uint64_t)seg_off[s] + lo;
+        const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15);
+        const uint32_t nch = (eff >> 4) + ((head + (eff & 15u) + 15u) >> 4);
+        const uint32_t last_end = ((head + (eff & 15u) + 15u) & 15u) + 1u;
+        const uint8_t* cb = a - head;
+        uint64_t lsum = 0;
+        for (uint32_t k0 = 0; k0 < nch; k0 += 64 * kWideU) {
+          u32x4 v[kWideU];
+#pragma unroll
+          for (int u = 0; u < kWideU; ++u)
+            if (u == 0 || k0 + 64u * u < nch)
+              v[u] = load_chunk(cb + 16ull * min(k0 + (uint32_t)(u * 64 + lane), nch - 1));
+          uint32_t part = 0;  // < kWideU * 2^19
+#pragma unroll
+          for (int u = 0; u < kWideU; ++u) {
+            if (u == 0 || k0 + 64u * u < nch) {
+              const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
+              const int lo_b = k == 0 ? (int)head : (k < nch ? 0 : 16);
+              const int hi_b = k + 1 < nch ? 16 : (k + 1 == nch ? (int)last_end : 0);
+              part += lut.sum_oc(v[u], lo_b, hi_b);
+            }
+          }
+          lsum += part;
+        }
+        if (((pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1u)
+          od += lsum;
+        else
+          ev += lsum;
+      }
+      pos += l;
+    }
+    const uint32_t e = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(ev), 0u), 63);
+    const uint32_t o = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(od), 0u), 63);
+    if (lane == 0) out[p] = finish((uint64_t)e + rot8(fold16(o)) + (seed ? seed[p] : 0u), flags);
+  }
+}
+
 template <typename OffT, typename LenT>
 int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
                     const uint32_t* pkt_seg, const uint32_t* len, const uint32_t* skip,
                     const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
                     uint32_t len_hint, hipStream_t stream) {
-  (void)len_hint;  // the chunk stream does not depend on segment lengths
   if (n == 0) return UINET_CKSUM_OK;
   const Tuning& tn = tuning();
   const uint8_t* b = static_cast<const uint8_t*>(base);
+  // Long segments on average (len_hint = mean segment bytes): a wave per packet.
+  if (tn.chains_wide == 2 || (tn.chains_wide == 0 && len_hint >= kWideHint)) {
+    uint64_t blocks = ((uint64_t)n + kWaves - 1) / kWaves;
+    const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
+    blocks = blocks > cap ? cap : blocks;
+    UINET_LAUNCH((k_chains_wide<OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, b,
+                 seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags);
+    return check_launch();
+  }
   // Tile of 32 packets, or 8 when 32 would give fewer than 16 tiles per CU
   // (5tso, 131 K packets, runs 0.8 % faster at 32: profiles/r01/ab/bpc_s6/tile).
   const int tile = tn.chains_tile ? tn.chains_tile : (n >= 32u * 4096u ? 32 : 8);

@@ -19,9 +19,10 @@ from test_gpu_parity import dev, host16, rand_arena
 pytestmark = pytest.mark.gpu
 
 DEFAULTS = {"blocks_per_cu": 0, "chains_pass": 2, "chains_long": 128, "chains_tile": 0,
-            "xcd_remap": 1, "spans_geo": 0, "spans_pipe": 1}
+            "xcd_remap": 1, "spans_geo": 0, "spans_pipe": 1, "chains_wide": 0}
 KNOBS = {"blocks_per_cu": [0, 0, 1, 3, 64], "chains_pass": [2, 2, 4], "chains_long": [128, 0, 16],
          "chains_tile": [0, 8, 32], "xcd_remap": [1, 0], "spans_pipe": [1, 1, 0],
+         "chains_wide": [0, 0, 1, 2],
          "spans_geo": [0] * 6 + [4 * 16 + 1, 4 * 16 + 2, 8 * 16 + 1, 8 * 16 + 2, 16 * 16 + 3,
                                  32 * 16 + 3, 64 * 16 + 2, 64 * 16 + 3, 64 * 16 + 9]}
 HINTS = (0, 64, 80, 200, 500, 1500, 4000, 9000)

@@ -884,6 +884,12 @@ def test_chains_beyond_4gib_window(torch_dev, ora):
         finally:
             u.set_tuning("chains_pass", 2)
         np.testing.assert_array_equal(host16(got), want)
+    # the wave-per-packet kernel over the same chains (mean segment >= 2 KiB picks it)
+    got = u.cksum_chains(d, dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
+                         dev(torch, pkt_seg.astype(np.int32)), skip=dev(torch, skip.astype(np.int32)),
+                         seed=dev(torch, seed.view(np.int32)), len_hint=4096)
+    assert "k_chains_wide" in u.last_kernel()
+    np.testing.assert_array_equal(host16(got), want)
     # spans and strided packets past the 4 GiB mark (64-bit offsets)
     off = rng.integers((1 << 32) - 4096, size - 10000, 3000).astype(np.int64)
     ln = rng.integers(0, 9000, 3000)

@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # min(16, hardware threads)
 DEFAULTS = {"blocks_per_cu": 0, "chains_pass": 2, "chains_long": 128, "chains_tile": 0,
             "xcd_remap": 1, "spans_geo": 0, "spans_pipe": 1,
-            "walk_prefetch": 1, "host_pin": 0, "multi_gather": 0,
+            "walk_prefetch": 1, "host_pin": 0, "multi_gather": 0, "chains_wide": 0,
             "host_threads": min(16, os.cpu_count() or 1)}
 
 
