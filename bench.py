@@ -192,7 +192,8 @@ def dispatched_kernel(cfg: str, api: str, w) -> str:
     launch_spans / launch_strided / launch_chains in libuinet_amd/csrc and the
     UINET_CKSUM_SPANS_PIPE / UINET_CKSUM_SPANS_GEO knobs)."""
     if cfg in CHAIN_CONFIGS:
-        return "k_chains_pipe"
+        wide = int(os.environ.get("UINET_CKSUM_CHAINS_WIDE", "0") or 0)
+        return "k_chains_wide" if wide == 2 or (wide == 0 and w["hint"] >= 2048) else "k_chains_pipe"
     pipe = int(os.environ.get("UINET_CKSUM_SPANS_PIPE", "1") or 1)
     geo = int(os.environ.get("UINET_CKSUM_SPANS_GEO", "0") or 0)
     mean = w["length"] if api == "strided" else w["hint"]
@@ -219,6 +220,7 @@ def dispatched_kernel(cfg: str, api: str, w) -> str:
 # only while they are byte-identical to the ones it was measured on.
 KERNEL_SOURCES = {
     "k_chains_pipe": ("cksum_chains.hip", "cksum_device.h"),
+    "k_chains_wide": ("cksum_chains.hip", "cksum_device.h"),
     "k_spans_lean": ("cksum_spans.hip", "cksum_device.h"),
     "k_spans_quad": ("cksum_spans.hip", "cksum_device.h"),
     "k_strided_dense": ("cksum_spans.hip", "cksum_device.h"),

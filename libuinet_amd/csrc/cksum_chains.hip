@@ -400,6 +400,25 @@ __global__ __launch_bounds__(kBlock) UINET_CHAINS_OCC void k_chains_pipe(const u
 }
 
 
+// A segment length read by a wave-uniform (scalar) load.  A packed u16 length
+// is taken out of its aligned 32-bit word: s_load has no 16-bit form, and a
+// vector load of it would share the vector memory counter with the packet
+// bytes in flight (a wait for it waits for them).  The word lies in the page
+// that holds the length.
+template <typename LenT>
+__device__ __forceinline__ uint32_t seg_len_at(const LenT* __restrict__ p, uint32_t s) {
+  if constexpr (sizeof(LenT) == 2) {
+    // the word pointer stays derived from the argument (no integer round
+    // trip), which is what lets the compiler keep the load scalar
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(p) >> 1) & 1u;
+    const uint32_t i = s + mis;
+    const uint32_t w = reinterpret_cast<const uint32_t*>(p - mis)[i >> 1];
+    return (i & 1u) ? w >> 16 : w & 0xffffu;
+  } else {
+    return (uint32_t)p[s];
+  }
+}
+
 // k_chains_wide: one wave per packet, for chains of few long segments (a TSO
 // engine's 40-B header mbuf + 9 KB payload slice, config 5tso).  The tile
 // kernel above streams such a segment with 2 chunks per lane in flight (its
@@ -431,43 +450,90 @@ __global__ __launch_bounds__(kBlock) void k_chains_wide(const uint8_t* __restric
     const uint32_t sk = pskip ? pskip[p] : 0u;
     const uint32_t ln = plen ? plen[p] : 0xffffffffu;
     uint64_t ev = 0, od = 0;  // this lane's chunk sums by logical parity
-    uint32_t pos = 0;         // chain offset of segment s
-    for (uint32_t s = S0; s < S1; ++s) {
-      const uint32_t l = (uint32_t)seg_len[s];
+    struct Seg {
+      const uint8_t* cb;
+      uint32_t head, nch, last_end;
+      bool rot;
+    };
+    // Segment s at chain offset pos, clipped to [sk, ln): nch 0 when empty.
+    // Descriptors are read by scalar loads (wave-uniform), so a read never
+    // waits behind packet-byte loads in the vector memory counter.
+    auto desc = [&](uint32_t s, uint32_t pos, uint32_t l) {
+      Seg g{nullptr, 0u, 0u, 0u, false};
       const uint32_t lo = sk > pos ? min(sk - pos, l) : 0u;
       const uint32_t hi = ln > pos ? min(ln - pos, l) : 0u;
       if (hi > lo) {
         const uint32_t eff = hi - lo;
         const uint8_t* a = base + (uint64_t)seg_off[s] + lo;
-        const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15);
-        const uint32_t nch = (eff >> 4) + ((head + (eff & 15u) + 15u) >> 4);
-        const uint32_t last_end = ((head + (eff & 15u) + 15u) & 15u) + 1u;
-        const uint8_t* cb = a - head;
-        uint64_t lsum = 0;
-        for (uint32_t k0 = 0; k0 < nch; k0 += 64 * kWideU) {
-          u32x4 v[kWideU];
-#pragma unroll
-          for (int u = 0; u < kWideU; ++u)
-            if (u == 0 || k0 + 64u * u < nch)
-              v[u] = load_chunk(cb + 16ull * min(k0 + (uint32_t)(u * 64 + lane), nch - 1));
-          uint32_t part = 0;  // < kWideU * 2^19
-#pragma unroll
-          for (int u = 0; u < kWideU; ++u) {
-            if (u == 0 || k0 + 64u * u < nch) {
-              const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
-              const int lo_b = k == 0 ? (int)head : (k < nch ? 0 : 16);
-              const int hi_b = k + 1 < nch ? 16 : (k + 1 == nch ? (int)last_end : 0);
-              part += lut.sum_oc(v[u], lo_b, hi_b);
-            }
-          }
-          lsum += part;
-        }
-        if (((pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1u)
-          od += lsum;
-        else
-          ev += lsum;
+        g.head = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15);
+        g.nch = (eff >> 4) + ((g.head + (eff & 15u) + 15u) >> 4);
+        g.last_end = ((g.head + (eff & 15u) + 15u) & 15u) + 1u;
+        g.cb = a - g.head;
+        g.rot = ((pos + lo - sk) ^ (uint32_t)reinterpret_cast<uintptr_t>(a)) & 1u;
       }
+      return g;
+    };
+    // chunk k's kept byte range [lo_b, hi_b) within segment g
+    auto lo_of = [](const Seg& g, uint32_t k) { return k == 0 ? (int)g.head : (k < g.nch ? 0 : 16); };
+    auto hi_of = [](const Seg& g, uint32_t k) {
+      return k + 1 < g.nch ? 16 : (k + 1 == g.nch ? (int)g.last_end : 0);
+    };
+    auto add = [&](bool rot, uint64_t x) {
+      if (rot) od += x; else ev += x;
+    };
+    // One round of a long segment from chunk k0: kWideU chunks per lane.
+    // `pre` runs between the loads and their sums (a short segment summed
+    // while these loads are in flight).
+    auto round = [&](const Seg& g, uint32_t k0, auto pre) {
+      u32x4 v[kWideU];
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u)
+        if (u == 0 || k0 + 64u * u < g.nch)
+          v[u] = load_chunk(g.cb + 16ull * min(k0 + (uint32_t)(u * 64 + lane), g.nch - 1));
+      pre();
+      uint32_t part = 0;  // < kWideU * 2^19
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u) {
+        if (u == 0 || k0 + 64u * u < g.nch) {
+          const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
+          part += lut.sum_oc(v[u], lo_of(g, k), hi_of(g, k));
+        }
+      }
+      add(g.rot, part);
+    };
+    auto rest = [&](const Seg& g) {
+      for (uint32_t k0 = 64 * kWideU; k0 < g.nch; k0 += 64 * kWideU) round(g, k0, [] {});
+    };
+    uint32_t pos = 0;  // chain offset of segment s
+    for (uint32_t s = S0; s < S1; ++s) {
+      const uint32_t l = seg_len_at(seg_len, s);
+      const Seg g = desc(s, pos, l);
       pos += l;
+      if (g.nch == 0) continue;
+      if (g.nch > 64) {  // long: rounds of kWideU chunks per lane
+        round(g, 0, [] {});
+        rest(g);
+        continue;
+      }
+      // short (one chunk per lane).  Followed by a long segment (a TSO
+      // header and its payload slice), the long one's descriptor is read
+      // while the short one's bytes are in flight, and its sum is added under
+      // the long one's first round.
+      const uint32_t k = (uint32_t)lane;
+      const u32x4 hv = load_chunk(g.cb + 16ull * min(k, g.nch - 1));
+      const uint32_t hs = lut.sum_oc(hv, lo_of(g, k), hi_of(g, k));
+      if (s + 1 < S1) {
+        const uint32_t l2 = seg_len_at(seg_len, s + 1);
+        const Seg g2 = desc(s + 1, pos, l2);
+        if (g2.nch > 64) {
+          pos += l2;
+          ++s;
+          round(g2, 0, [&] { add(g.rot, hs); });
+          rest(g2);
+          continue;
+        }
+      }
+      add(g.rot, hs);
     }
     const uint32_t e = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(ev), 0u), 63);
     const uint32_t o = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(od), 0u), 63);

@@ -16,5 +16,5 @@ for c in 5tso 3tx 3; do
   step ab_$c 300 python3 tools/ab.py --config $c --rounds 8 --variants chains_wide=1 chains_wide=2 chains_wide=1,desc=1 chains_wide=2,desc=1
 done
 step bench_c5tso 200 python3 bench.py --config 5tso --steps 50 --warmup 20 --host-offload off
-step trace_c5tso 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_c5tso" -o run -- python3 bench.py --config 5tso --steps 20 --warmup 5 --cpu-baseline off --host-offload off
+step trace_c5tso 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_c5tso" -o run --output-format csv -- python3 bench.py --config 5tso --steps 20 --warmup 5 --cpu-baseline off --host-offload off
 echo "== done"
