@@ -439,12 +439,14 @@ __global__ __launch_bounds__(kBlock) void k_chains_wide(const uint8_t* __restric
                                                        const uint32_t* __restrict__ pskip,
                                                        const uint32_t* __restrict__ seed,
                                                        uint16_t* __restrict__ out, uint32_t n,
-                                                       uint32_t flags) {
+                                                       uint32_t flags, uint32_t remap) {
   __shared__ MaskLut lut;
   lut.init();
   const int lane = threadIdx.x & 63;
   const uint32_t wstride = gridDim.x * kWaves;
-  for (uint32_t p = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  // XCD-banded packet order (knob xcd_remap): neighbouring packets share
+  // descriptor and header lines, fetched once into one XCD's L2
+  for (uint32_t p = __builtin_amdgcn_readfirstlane(logical_block(remap) * kWaves + (threadIdx.x >> 6));
        p < n; p += wstride) {
     const uint32_t S0 = pkt_seg[p], S1 = pkt_seg[p + 1];
     const uint32_t sk = pskip ? pskip[p] : 0u;
@@ -555,7 +557,7 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
     const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
     blocks = blocks > cap ? cap : blocks;
     UINET_LAUNCH((k_chains_wide<OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0, stream, b,
-                 seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags);
+                 seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, (uint32_t)tn.xcd_remap);
     return check_launch();
   }
   // Tile of 32 packets, or 8 when 32 would give fewer than 16 tiles per CU
