@@ -236,7 +236,9 @@ int uinet_cksum_strided(const void *base, uint64_t stride, uint32_t len,
  * in_cksum_skip(chain_i, len[i], skip[i]) exactly as in_cksum.c:193-232
  * defines it (len counts from the chain start; len NULL = whole chain, skip
  * NULL = 0), plus seed[i] (NULL = 0) before folding.  `len_hint` is the mean
- * SEGMENT length here. */
+ * SEGMENT length here: 2048 or more picks one wave per packet (chains of few
+ * long segments, a TSO header + payload slice), less the 32-packet tile
+ * kernel (knob "chains_wide"). */
 int uinet_cksum_chains(const void *base, const uint64_t *seg_off,
     const uint32_t *seg_len, const uint32_t *pkt_seg, const uint32_t *len,
     const uint32_t *skip, const uint32_t *seed, uint16_t *out, uint32_t n,
