@@ -193,7 +193,8 @@ def dispatched_kernel(cfg: str, api: str, w) -> str:
     UINET_CKSUM_SPANS_PIPE / UINET_CKSUM_SPANS_GEO knobs)."""
     if cfg in CHAIN_CONFIGS:
         wide = int(os.environ.get("UINET_CKSUM_CHAINS_WIDE", "0") or 0)
-        return "k_chains_wide" if wide == 2 or (wide == 0 and w["hint"] >= 2048) else "k_chains_pipe"
+        pick = wide == 2 or (wide == 0 and 4096 <= w["hint"] <= 9216)
+        return "k_chains_wide" if pick else "k_chains_pipe"
     pipe = int(os.environ.get("UINET_CKSUM_SPANS_PIPE", "1") or 1)
     geo = int(os.environ.get("UINET_CKSUM_SPANS_GEO", "0") or 0)
     mean = w["length"] if api == "strided" else w["hint"]

@@ -172,7 +172,7 @@ int uinet_cksum_device_ok(void);
  *                     registered memory: 1 (default) the GPU walks the chains,
  *                     the host only writes the jobs; 0 the host walks them
  *   "chains_wide"     chain API: 0 (default) one wave per packet when
- *                     len_hint (mean segment bytes) is >= 2048, else the
+ *                     len_hint (mean segment bytes) is 4096-9216, else the
  *                     tile kernel; 1 = always the tile kernel, 2 = always
  *                     one wave per packet
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
@@ -236,8 +236,8 @@ int uinet_cksum_strided(const void *base, uint64_t stride, uint32_t len,
  * in_cksum_skip(chain_i, len[i], skip[i]) exactly as in_cksum.c:193-232
  * defines it (len counts from the chain start; len NULL = whole chain, skip
  * NULL = 0), plus seed[i] (NULL = 0) before folding.  `len_hint` is the mean
- * SEGMENT length here: 2048 or more picks one wave per packet (chains of few
- * long segments, a TSO header + payload slice), less the 32-packet tile
+ * SEGMENT length here: 4096-9216 picks one wave per packet (segments of a
+ * jumbo frame or a TSO payload slice), anything else the 32-packet tile
  * kernel (knob "chains_wide"). */
 int uinet_cksum_chains(const void *base, const uint64_t *seg_off,
     const uint32_t *seg_len, const uint32_t *pkt_seg, const uint32_t *len,

@@ -52,7 +52,11 @@ typedef unsigned short us16x2 __attribute__((ext_vector_type(2)));
 #endif
 constexpr int kLongU = UINET_CHAINS_LONGU;  // chunks in flight per lane on a long segment
 constexpr uint32_t kListMax = 1024;  // longest segment (chunks) the chunk list takes
-constexpr uint32_t kWideHint = 2048;  // mean segment bytes from which k_chains_wide runs
+// Mean segment bytes (len_hint) for which k_chains_wide runs: a segment that
+// fits one of its 9-KiB rounds (a jumbo frame, a TSO payload slice).  Longer
+// segments take serial rounds, and 1-2 KiB ones leave it per-packet bound,
+// where the tile kernel is faster (tools/chains_cross.py, profiles/r05/r05cross*).
+constexpr uint32_t kWideHintLo = 4096, kWideHintHi = 64 * 9 * 16;
 
 // 16-B raw buffer load, non-temporal (aux bit 1), from a resource spanning
 // 4 GiB: one VGPR of offset instead of a 64-bit address per chunk.
@@ -551,8 +555,9 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
   if (n == 0) return UINET_CKSUM_OK;
   const Tuning& tn = tuning();
   const uint8_t* b = static_cast<const uint8_t*>(base);
-  // Long segments on average (len_hint = mean segment bytes): a wave per packet.
-  if (tn.chains_wide == 2 || (tn.chains_wide == 0 && len_hint >= kWideHint)) {
+  // Segments of 4-9 KiB on average (len_hint = mean segment bytes): a wave per packet.
+  if (tn.chains_wide == 2 ||
+      (tn.chains_wide == 0 && len_hint >= kWideHintLo && len_hint <= kWideHintHi)) {
     uint64_t blocks = ((uint64_t)n + kWaves - 1) / kWaves;
     const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
     blocks = blocks > cap ? cap : blocks;

@@ -21,7 +21,7 @@ struct Tuning {
                        // wave-wide (0 = never)
   int chains_tile;     // flat chains: packets per wave tile, 0 = auto, 8, 32
   int chains_wide;     // chains: 0 = a wave per packet (k_chains_wide) when the mean
-                       // segment is >= 2 KiB, 1 = never, 2 = always
+                       // segment is 4-9 KiB, 1 = never, 2 = always
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
   int spans_pipe;      // span kernel family: 1 k_spans_lean / k_spans_quad (persistent,
                        // mask-free whole chunks), 0 one-shot k_spans

@@ -5,7 +5,7 @@ segments, hundreds of segments per chain, len / skip cutting inside and on
 segment boundaries, len <= skip, segments longer than one 9 KiB load round,
 seeds, UDP and no-complement flags, wide and packed descriptors -- bit-exact
 against the oracle with the kernel forced (knob chains_wide = 2) and picked by
-the mean segment length (len_hint >= 2048)."""
+the mean segment length (len_hint 4096-9216)."""
 from __future__ import annotations
 
 import zlib
@@ -88,9 +88,9 @@ def test_chains_wide_matches_oracle(wide, ora, shape, max_segs, desc):
 
 
 def test_chains_wide_picked_by_hint(torch_dev, ora):
-    """Auto (chains_wide 0): a mean segment of 2 KiB or more takes the
-    wave-per-packet kernel, shorter ones the tile kernel; both equal the
-    oracle on the same TSO-shaped batch."""
+    """Auto (chains_wide 0): a mean segment of 4-9 KiB takes the
+    wave-per-packet kernel, shorter and longer ones the tile kernel; both
+    equal the oracle on the same TSO-shaped batch."""
     torch = torch_dev
     from libuinet_amd.workloads import chain_layout, materialize_device
 
@@ -98,7 +98,8 @@ def test_chains_wide_picked_by_hint(torch_dev, ora):
     lay = w["layout"]
     want = ora.chains(w["arena"].cpu().numpy(), lay["seg_off"], lay["seg_len"], lay["pkt_seg"],
                       length=lay["lens"], skip=lay["skip"], seed=lay["seed"])
-    for hint, kern in ((w["mean_seg"], "k_chains_wide"), (300, "k_chains_pipe")):
+    for hint, kern in ((w["mean_seg"], "k_chains_wide"), (300, "k_chains_pipe"),
+                       (16384, "k_chains_pipe")):
         got = u.cksum_chains(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"], length=w["len"],
                              skip=w["skip"], seed=w["seed"], len_hint=int(hint))
         assert kern in u.last_kernel(), (hint, u.last_kernel())
