@@ -104,3 +104,25 @@ def test_chains_wide_picked_by_hint(torch_dev, ora):
                              skip=w["skip"], seed=w["seed"], len_hint=int(hint))
         assert kern in u.last_kernel(), (hint, u.last_kernel())
         np.testing.assert_array_equal(host16(got), want)
+
+
+def test_chains_wide_packed_lengths_off_word(wide, ora):
+    """Packed u16 lengths whose array starts 2 B past a 4-B boundary: the
+    kernel reads each length out of its aligned 32-bit word (seg_len_at), so
+    both halves of a word and the array's first and last entries are checked
+    against the oracle."""
+    torch = wide
+    rng = np.random.default_rng(77)
+    arena = rand_arena(1 << 22, 62)
+    n = 1500
+    seg_off, seg_len, pkt_seg = _layout(rng, n, arena.size, 3,
+                                        lambda s: rng.integers(0, 9300, s))
+    so, sl = u.pack_segments(seg_off, seg_len.astype(np.int32))
+    big = torch.zeros(sl.size + 1, dtype=torch.int16, device="cuda")
+    big[1:] = dev(torch, sl).to(torch.int16)
+    d_sl = big[1:]  # storage offset 1: the array starts 2 B into a word
+    assert d_sl.data_ptr() % 4 == 2
+    want = ora.chains(arena, seg_off, seg_len, pkt_seg)
+    got = u.cksum_chains(dev(torch, arena), dev(torch, so), d_sl, dev(torch, pkt_seg.astype(np.int32)))
+    assert "k_chains_wide" in u.last_kernel()
+    np.testing.assert_array_equal(host16(got), want)
