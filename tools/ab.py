@@ -35,13 +35,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--variants", nargs="+", required=True)
+    ap.add_argument("--packets", type=int, default=None, help="batch size (default: the config's)")
     a = ap.parse_args()
     import torch
 
     import bench
     import libuinet_amd as u
 
-    w = bench.build_workload(a.config, None, 0)
+    w = bench.build_workload(a.config, a.packets, 0)
     out = torch.empty(w["n"], dtype=torch.uint16, device="cuda")
     s = torch.cuda.current_stream()
     if a.config in bench.CHAIN_CONFIGS:
