@@ -437,18 +437,21 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
         keep.update(host=host, ch=ch, args=args,
                     pseudo=cfg in ("5", "5tso"))
     gib = w["bytes"] / 2**30
-    runs, spread = {}, {}
+    runs, spread, read = {}, {}, {}
     if timer is not None:
         # median of 5 single passes per (threads, placement): the threads pinned
-        # to the first CPUs of the process mask, and left to the scheduler (on
-        # the GPU box's 256-CPU mask floating threads spread over more caches
-        # and memory channels and ran 1.3-2x faster, profiles/r02/host_pin/).
-        # One best-of-5 on a shared box once read an impossible 1.7 TB/s
-        # (profiles/r02/final/NOTES.md), hence medians.  `threads` is the box's
-        # CPU share (16 per GPU): the rest of the mask belongs to the other
-        # GPUs' jobs on the machine.
-        # plus every CPU of the process mask (SURVEY.md 8d "1 thread, then all
-        # host cores"; one thread per CPU, at most the harness's 256)
+        # to the first CPUs of the process mask, and left to the scheduler.
+        # `threads` is the box's CPU share (16 per GPU): the rest of the mask
+        # belongs to the other GPUs' jobs on the machine; plus every CPU of the
+        # process mask (SURVEY.md 8d "1 thread, then all host cores"; one
+        # thread per CPU, at most 256).  Every pass is max(worker end) -
+        # min(worker start), stamped by the workers themselves
+        # (ref_harness.c): round 5 stamped on the main thread, which a busy
+        # mask scheduled late, and read passes of 1.3-2.3 TB/s, above the
+        # host's memory bandwidth.  Beside each checksum setting, 5 passes of a
+        # plain streaming read of the same host bytes with the same threads
+        # and placement: the host's read bandwidth, which no checksum pass can
+        # beat (`within_read_ceiling`).
         outs = []
         n_all = min(len(allowed), 256)
         for nt in sorted({1, threads, n_all}):
@@ -458,6 +461,8 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
                 runs[f"{nt}_{placement}"] = float(np.median([r[0] for r in rr]))
                 spread[f"{nt}_{placement}"] = (min(r[0] for r in rr), max(r[0] for r in rr))
                 outs.append(rr[-1][1])
+                rd = [R.time_read(host, nthreads=nt, cpus=pin, reps=1) for _ in range(5)]
+                read[f"{nt}_{placement}"] = (float(np.median(rd)), min(rd))
         best = min((k for k in runs if k.startswith(f"{threads}_")), key=runs.get)
         tn = runs[best]
         t1 = min(runs["1_pinned"], runs["1_floating"])
@@ -474,6 +479,10 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
     # from box to box (64.8 .. 271.2 GiB/s for one command on one CPU model,
     # VERDICT r03); the 1-thread figure is the stable comparison
     minmax = {k: [round(gib / hi, 3), round(gib / lo, 3)] for k, (lo, hi) in spread.items()}
+    host_gib = host.nbytes / 2**30
+    read_gibs = {k: round(host_gib / med, 3) for k, (med, _) in read.items()}
+    ceiling = round(max((host_gib / best_t for _, best_t in read.values()), default=0.0), 3)
+    fastest = max((v[1] for v in minmax.values()), default=0.0)
     return {
         "value": round(gib / tn, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
         "cpu_model": cpu_model(),
@@ -483,8 +492,9 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
                    + ", ".join(f"{k.replace('_', ' threads ')} {v}" for k, v in rates.items())
                    + f"); value = {best.replace('_', ' threads ')} (its 5 passes: "
                    + "{}-{} GiB/s".format(*minmax[best])
-                   + f"; the 1-thread figure is the stable comparison); results bit-identical to "
-                   f"the GPU in every run: {parity}"),
+                   + f"); every pass max(worker end) - min(worker start); host streaming-read "
+                   f"ceiling {ceiling} GiB/s; results bit-identical to the GPU in every run: "
+                   f"{parity}"),
         "runs_gibs": rates,
         "runs_minmax_gibs": minmax,
         "value_from": best,
@@ -497,6 +507,13 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
         "all_cores_threads": n_all,
         "all_cores_from": best_all,
         "mask_cpus": len(allowed),
+        # the host's streaming-read rate over the same host bytes (the arena)
+        # per thread count and placement (median of 5), and its fastest pass:
+        # the ceiling every checksum pass above must stay under
+        "host_read_gibs": read_gibs or None,
+        "host_read_ceiling_gibs": ceiling or None,
+        "fastest_pass_gibs": fastest,
+        "within_read_ceiling": (fastest <= ceiling) if ceiling else None,
         "bit_identical_to_gpu": parity,
     }
 

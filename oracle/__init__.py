@@ -180,7 +180,8 @@ class Reference:
             "refh_pseudo_batch": (None, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32]),
             "refh_hdr_batch": (None, [_vp, _vp, _i32]),
             "refh_time_batch": (ctypes.c_double, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
-                                                  _i32, _vp, _i32]),
+                                                  _i32, _vp, _i32, _vp]),
+            "refh_time_read": (ctypes.c_double, [_vp, ctypes.c_long, _i32, _vp, _i32, _vp, _vp]),
             "refh_in6_cksum": (_i32, [_vp, _u8, _u32, _u32]),
             "refh_in6_cksum_pseudo": (_i32, [_vp, _u32, _u8, _u16]),
             "refh_in6_batch": (None, [_vp, _vp, _vp, _vp, _vp, _i32]),
@@ -243,27 +244,48 @@ class Reference:
         self.L.refh_in6_batch(_p(heads), *[_p(a) for a in arrs], _p(out), n)
         return out
 
-    def time_skip(self, heads, length, skip, nthreads=1, cpus=None, reps=5):
-        """Best-of-``reps`` wall seconds of in_cksum_skip over the batch."""
+    @staticmethod
+    def _stamps(nthreads, with_stamps):
+        return np.zeros(2 * max(1, nthreads), np.float64) if with_stamps else None
+
+    def time_skip(self, heads, length, skip, nthreads=1, cpus=None, reps=5, stamps=False):
+        """Best-of-``reps`` pass, seconds, of in_cksum_skip over the batch:
+        every worker stamps its own start and end, a pass is max(end) -
+        min(start).  Returns (t, out) or, with ``stamps``, (t, out, the last
+        pass's per-worker [start, end] pairs)."""
         heads = _c(heads, np.uint64)
         n = heads.size
         length, skip = _c(length, np.int32, n), _c(skip, np.int32, n)
         out = np.zeros(n, np.uint16)
         cpus_a = None if cpus is None else np.ascontiguousarray(cpus, dtype=np.int32)
+        st = self._stamps(nthreads, stamps)
         t = self.L.refh_time_batch(0, _p(heads), _p(length), _p(skip), 0, 0, 0, _p(out), n,
-                                   nthreads, _p(cpus_a), reps)
-        return t, out
+                                   nthreads, _p(cpus_a), reps, _p(st))
+        return (t, out, st.reshape(-1, 2)[:nthreads]) if stamps else (t, out)
 
-    def time_pseudo(self, heads, plen, off0, src, dst, proto, nthreads=1, cpus=None, reps=5):
+    def time_pseudo(self, heads, plen, off0, src, dst, proto, nthreads=1, cpus=None, reps=5,
+                    stamps=False):
         heads = _c(heads, np.uint64)
         n = heads.size
         arrs = [_c(plen, np.int32, n), _c(off0, np.int32, n), _c(src, np.uint32, n),
                 _c(dst, np.uint32, n), _c(proto, np.uint8, n)]
         out = np.zeros(n, np.uint16)
         cpus_a = None if cpus is None else np.ascontiguousarray(cpus, dtype=np.int32)
+        st = self._stamps(nthreads, stamps)
         t = self.L.refh_time_batch(1, _p(heads), *[_p(a) for a in arrs], _p(out), n, nthreads,
-                                   _p(cpus_a), reps)
-        return t, out
+                                   _p(cpus_a), reps, _p(st))
+        return (t, out, st.reshape(-1, 2)[:nthreads]) if stamps else (t, out)
+
+    def time_read(self, buf: np.ndarray, nthreads=1, cpus=None, reps=1, stamps=False):
+        """The host's read bandwidth over ``buf``: best-of-``reps`` pass,
+        seconds, of a plain streaming 64-bit sum on ``nthreads`` threads,
+        timed like time_skip (ref_harness.c refh_time_read)."""
+        buf = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+        cpus_a = None if cpus is None else np.ascontiguousarray(cpus, dtype=np.int32)
+        st = self._stamps(nthreads, stamps)
+        sink = np.zeros(1, np.uint64)
+        t = self.L.refh_time_read(_p(buf), buf.size, nthreads, _p(cpus_a), reps, _p(st), _p(sink))
+        return (t, st.reshape(-1, 2)[:nthreads]) if stamps else t
 
 
 def have_reference() -> bool:
