@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--desc", choices=["wide", "packed"], default="wide",
                     help="12-B wide (uinet_cksum_chains / uinet_cksum_spans) or packed "
                     "6-B (uinet_cksum_chains32 / uinet_cksum_spans32) descriptors")
+    ap.add_argument("--form", choices=["seglist", "mbufs"], default="seglist",
+                    help="chain configs (3, 3tx, 5tso): a segment list resolved from the chains "
+                    "(uinet_cksum_chains) or the struct mbuf chains themselves in HBM, walked "
+                    "on the GPU (uinet_cksum_mbufs)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--host-offload", choices=["auto", "off"], default="auto",
@@ -162,9 +166,13 @@ def build_workload(cfg: str, n, rank: int, world: int = 1):
     return w
 
 
-def make_launch(cfg: str, w, api: str, out, desc: str = "wide", flags: int = 0):
+def make_launch(cfg: str, w, api: str, out, desc: str = "wide", flags: int = 0,
+                form: str = "seglist"):
     import libuinet_amd as u
 
+    if cfg in CHAIN_CONFIGS and form == "mbufs":
+        return lambda s: u.cksum_mbufs(w["heads"], length=w["len"], skip=w["skip"],
+                                       seed=w.get("seed"), out=out, flags=flags, stream=s)
     if cfg in CHAIN_CONFIGS:
         so, sl = (w["seg_off"], w["seg_len"]) if desc == "wide" else w["packed"]
         return lambda s: u.cksum_chains(w["arena"], so, sl, w["pkt_seg"],
@@ -179,42 +187,14 @@ def make_launch(cfg: str, w, api: str, out, desc: str = "wide", flags: int = 0):
                                    len_hint=w["hint"], stream=s)
 
 
-def kernel_name(cfg: str, api: str, desc: str = "wide") -> str:
+def kernel_name(cfg: str, api: str, desc: str = "wide", form: str = "seglist") -> str:
+    if cfg in CHAIN_CONFIGS and form == "mbufs":
+        return "k_mbufs"
     if cfg in CHAIN_CONFIGS:
         return "k_chains32" if desc == "packed" else "k_chains"
     if api == "strided":
         return "k_strided"
     return "k_spans32" if desc == "packed" else "k_spans"
-
-
-def dispatched_kernel(cfg: str, api: str, w) -> str:
-    """The kernel family the engine launches for this line (mirrors
-    launch_spans / launch_strided / launch_chains in libuinet_amd/csrc and the
-    UINET_CKSUM_SPANS_PIPE / UINET_CKSUM_SPANS_GEO knobs)."""
-    if cfg in CHAIN_CONFIGS:
-        wide = int(os.environ.get("UINET_CKSUM_CHAINS_WIDE", "0") or 0)
-        pick = wide == 2 or (wide == 0 and 4096 <= w["hint"] <= 9216)
-        return "k_chains_wide" if pick else "k_chains_pipe"
-    pipe = int(os.environ.get("UINET_CKSUM_SPANS_PIPE", "1") or 1)
-    geo = int(os.environ.get("UINET_CKSUM_SPANS_GEO", "0") or 0)
-    mean = w["length"] if api == "strided" else w["hint"]
-    if (api == "strided" and pipe == 1 and not geo and 32 <= w["stride"] <= 256
-            and w["length"] <= w["stride"] and 4 * (w["stride"] - w["length"]) <= w["stride"]
-            and (w["base"] | w["stride"]) % 16):
-        return "k_strided_dense"  # launch_strided: small packets off 16-B alignment
-    g = 4 if mean <= 64 else 8 if mean <= 224 else 16 if mean <= 720 else 32 if mean <= 1520 else 64
-    u = 2 if g == 4 else 9 if mean > 6144 else 3
-    if api == "strided" and mean <= 64 and (w["base"] | w["stride"]) % 16 == 0:
-        u = 1
-    if geo:
-        g, u = geo // 16, geo % 16
-    if g >= 32:
-        if pipe == 1 and u in (3, 9):
-            return "k_spans_lean"
-        return "k_spans"
-    if g == 4 and pipe == 1 and (api == "spans" or u == 1):
-        return "k_spans_quad"
-    return "k_spans"
 
 
 # The sources each kernel family is compiled from: a FETCH_SIZE entry counts
@@ -226,6 +206,7 @@ KERNEL_SOURCES = {
     "k_spans_quad": ("cksum_spans.hip", "cksum_device.h"),
     "k_strided_dense": ("cksum_spans.hip", "cksum_device.h"),
     "k_spans": ("cksum_kernels.hip", "cksum_device.h"),
+    "k_mbufs": ("cksum_mbufs.hip", "cksum_device.h", "walk_xlate.h"),
 }
 
 
@@ -279,7 +260,7 @@ def load_traffic(path: str, key: str, kernel: str):
     return float(e["hbm_read_bytes_per_launch"]), src
 
 
-def layout_floor_line(cfg: str, w, desc: str, kms) -> dict:
+def layout_floor_line(cfg: str, w, desc: str, kms, form: str = "seglist") -> dict:
     """Chain configs: the layout's HBM-traffic floor (distinct 128-B lines
     holding a summed byte + the descriptors the kernel reads) and the kernel's
     rate measured against it, beside the algorithmic roofline."""
@@ -289,11 +270,21 @@ def layout_floor_line(cfg: str, w, desc: str, kms) -> dict:
     skip = lay.get("skip")
     if skip is None:  # config 3: in_cksum_skip(m, len, 20)
         skip = np.full(w["n"], 20, np.int64)
+    seeded = w.get("seed") is not None
     fl = W.layout_floor(lay["seg_off"], lay["seg_len"], lay["pkt_seg"], lay["lens"], skip,
-                        w.get("seed") is not None, 128, 6 if desc == "packed" else 12)
-    achieved = fl["floor_bytes"] / (float(kms.mean()) * 1e-3) / 1e9
-    return {"bytes": fl["floor_bytes"], "line": 128,
-            "over_algorithmic": round(fl["floor_bytes"] / w["bytes"], 4),
+                        seeded, 128, 6 if desc == "packed" else 12)
+    floor = fl["floor_bytes"]
+    extra = {}
+    if form == "mbufs":
+        # no descriptors: the packet bytes' lines, one 128-B line per mbuf
+        # header the walk reads (records 256 B apart: a line each), and the
+        # jobs (head u64, len, skip [, seed] per packet)
+        walked = W.mbufs_walked(lay["seg_len"], lay["pkt_seg"], lay["lens"], skip)
+        floor = fl["arena_bytes"] + 128 * walked + w["n"] * (16 + (4 if seeded else 0))
+        extra = {"mbufs_walked": walked, "header_line_bytes": 128 * walked}
+    achieved = floor / (float(kms.mean()) * 1e-3) / 1e9
+    return {"bytes": floor, "line": 128, **extra,
+            "over_algorithmic": round(floor / w["bytes"], 4),
             "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4)}
 
 
@@ -718,7 +709,13 @@ def run(args, distributed: bool, wd):
         w["packed"] = u.pack_segments(w["seg_off"], w["seg_len"])
     elif args.desc == "packed" and args.api == "spans":
         w["packed"] = u.pack_segments(w["off"], w["len"])
-    launches = [make_launch(args.config, w, args.api, o, args.desc) for o in outs]
+    if args.form == "mbufs" and args.config in CHAIN_CONFIGS:
+        import libuinet_amd.workloads as W
+
+        # the same chains as struct mbufs in HBM (records in chain order)
+        w.update(W.device_mbufs(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"]))
+        w["desc"] += "; as struct mbuf chains in HBM, walked on the GPU (m_next / m_data / m_len)"
+    launches = [make_launch(args.config, w, args.api, o, args.desc, form=args.form) for o in outs]
     counts = [n] * world
     rg = ResultGather(counts, "cuda", depth=NBUF) if distributed else None
     K, Wm = args.steps, args.warmup
@@ -791,9 +788,11 @@ def run(args, distributed: bool, wd):
         total_bytes = w["bytes"] * world * K
         value = total_bytes / elapsed / 2**30
         achieved = w["bytes"] / (kms.mean() * 1e-3) / 1e9
-        key = f"{kernel_name(args.config, args.api, args.desc)}:config{args.config}:{n}"
-        launched = short_kernel(u.last_kernel())  # the instantiation that really ran
-        kern = launched.split("<")[0] or dispatched_kernel(args.config, args.api, w)
+        key = f"{kernel_name(args.config, args.api, args.desc, args.form)}:config{args.config}:{n}"
+        # the instantiation that really ran (never a re-derivation of the C
+        # dispatch rule: a knob set at run time would fool that)
+        launched = short_kernel(u.last_kernel())
+        kern = launched.split("<")[0]
         traffic, traffic_src = load_traffic(args.pmc, key, launched)
         result = {
             "metric": metric_name(),
@@ -815,8 +814,8 @@ def run(args, distributed: bool, wd):
                 "algorithmic_bytes_per_gpu": w["bytes"],
                 "api": {"spans": "uinet_cksum_spans" + ("32" if args.desc == "packed" else ""),
                         "strided": "uinet_cksum_strided"}[args.api]
-                if args.config not in CHAIN_CONFIGS else
-                {"wide": "uinet_cksum_chains", "packed": "uinet_cksum_chains32"}[args.desc],
+                if args.config not in CHAIN_CONFIGS else "uinet_cksum_mbufs" if args.form == "mbufs"
+                else {"wide": "uinet_cksum_chains", "packed": "uinet_cksum_chains32"}[args.desc],
                 "parallelism": f"dp{world} packet shards" + (
                     f" + {'RCCL' if backend == 'nccl' else backend} gather of u16 results, "
                     "overlapped with the next step's kernel" if distributed else ""),
@@ -838,7 +837,8 @@ def run(args, distributed: bool, wd):
             },
         }
         if args.config in CHAIN_CONFIGS:
-            result["roofline"]["layout_floor"] = layout_floor_line(args.config, w, args.desc, kms)
+            result["roofline"]["layout_floor"] = layout_floor_line(args.config, w, args.desc, kms,
+                                                                   args.form)
         if distributed:
             # rank 0's kernel is the roofline above; these are every rank's
             result["ranks"] = rank_fields(rank_stats, w["bytes"], elapsed / K * 1e3)

@@ -254,6 +254,30 @@ int uinet_cksum_chains32(const void *base, const uint32_t *seg_off,
     const uint32_t *skip, const uint32_t *seed, uint16_t *out, uint32_t n,
     uint32_t flags, uint32_t len_hint, void *stream);
 
+/* Chained packets as struct mbuf chains that live in HBM (config 3 "as
+ * chained mbufs with m_next scatter"): heads[i] is the device address of
+ * packet i's first mbuf, and every m_next and m_data in the chains is a
+ * device address too, used as is (the mbufs and their bytes were allocated
+ * in device memory).  out[i] is in_cksum_skip(heads[i], len[i], skip[i])
+ * exactly as in_cksum.c:193-232 defines it -- the GPU follows m_next /
+ * m_data / m_len (sys/sys/mbuf.h:90-98) as far as the reference does -- plus
+ * seed[i] (NULL = 0) before folding; len NULL = the whole chain, skip NULL =
+ * 0.  The in_cksum_pseudo_header form is in_cksum_skip(m, off0 + plen, off0)
+ * with the folded pseudo-header sum as seed (when off0 lies in the first
+ * mbuf, in_cksum.c:254-256).  One launch walks and folds; nothing else is
+ * allocated or written.  `status` (a device u32, may be NULL) receives the
+ * OR of UINET_CKSUM_MBUF_* bits for inputs outside the reference's contract;
+ * it is never cleared here.  The chains are trusted as the reference trusts
+ * them: every pointer the walk reaches must be readable device memory. */
+#define UINET_CKSUM_MBUF_TRUNC  0x1u /* a chain of more than UINET_CKSUM_MBUF_HOPS_MAX
+                                        mbufs: summed up to there */
+#define UINET_CKSUM_MBUF_BADLEN 0x2u /* a negative m_len: the chain ends there */
+#define UINET_CKSUM_MBUF_BADARG 0x4u /* a negative skip: the packet sums nothing */
+#define UINET_CKSUM_MBUF_HOPS_MAX 0x20000u
+int uinet_cksum_mbufs(const struct mbuf *const *heads, const int32_t *len,
+    const int32_t *skip, const uint32_t *seed, uint16_t *out, uint32_t n,
+    uint32_t flags, uint32_t *status, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* 2c. Host-mbuf batch API (synchronous; for the driver RX/TX batch hooks)   */
 /*                                                                          */

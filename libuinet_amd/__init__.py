@@ -9,7 +9,8 @@ the reference KPI of /root/reference/sys/amd64/include/in_cksum.h:44,76-83:
 * host-mbuf batches: :func:`in_cksum_skip_batch`, :func:`in_cksum_pseudo_header_batch`,
   :func:`in_cksum_hdr_batch`;
 * the device-resident hot path over HBM buffers held in torch tensors:
-  :func:`cksum_spans`, :func:`cksum_strided`, :func:`cksum_chains`.
+  :func:`cksum_spans`, :func:`cksum_strided`, :func:`cksum_chains`, and
+  :func:`cksum_mbufs` over struct mbuf chains that live in HBM.
 
 Everything that touches packet bytes runs in the HIP library
 ``libuinet_amd/libuinet_cksum.so``; if it is missing or no gfx950 device is
@@ -31,7 +32,8 @@ __all__ = [
     "in_cksum_pseudo_header_batch", "in_cksum_hdr_batch", "cksum_spans", "cksum_strided",
     "cksum_chains", "pack_segments", "F_UDP", "F_NO_COMPLEMENT", "MbufChains", "MBUF_DTYPE", "MSIZE",
     "SEED_BASE", "aligned_empty", "splitmix64_bytes", "EXPORTED_SYMBOLS", "cksum_spans_multi",
-    "in_cksum_skip_batch_multi", "host_cpu",
+    "in_cksum_skip_batch_multi", "host_cpu", "cksum_mbufs", "MBUF_TRUNC", "MBUF_BADLEN",
+    "MBUF_BADARG", "MBUF_HOPS_MAX",
 ]
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libuinet_cksum.so")
@@ -53,8 +55,12 @@ EXPORTED_SYMBOLS = (
     "uinet_cksum_rx_offload", "uinet_cksum_tx_offload",
     "in6_cksum", "in6_cksum_pseudo", "in6_cksum_batch",
     "uinet_cksum_spans_multi", "uinet_cksum_multi_last_gather", "in_cksum_skip_batch_multi",
-    "uinet_cksum_host_cpu",
+    "uinet_cksum_host_cpu", "uinet_cksum_mbufs",
 )
+
+# uinet_cksum_mbufs status bits and hop bound (include/uinet_cksum.h section 2b).
+MBUF_TRUNC, MBUF_BADLEN, MBUF_BADARG = 0x1, 0x2, 0x4
+MBUF_HOPS_MAX = 0x20000
 
 # Driver offload status bits (include/uinet_cksum.h section 2d).
 RX_IPV4, RX_IP_OK, RX_L4, RX_L4_OK, RX_NOSUM, RX_FRAG = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
@@ -123,6 +129,7 @@ def lib() -> ctypes.CDLL:
         "uinet_cksum_multi_last_gather": (_i32, []),
         "in_cksum_skip_batch_multi": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i32]),
         "uinet_cksum_host_cpu": (_i32, [_vp, _i32]),
+        "uinet_cksum_mbufs": (_i32, [_vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -373,6 +380,33 @@ def cksum_chains(base, seg_off, seg_len, pkt_seg, length=None, skip=None, seed=N
     _check(fn, getattr(lib(), fn)(
         _dp(base), _dp(seg_off), _dp(seg_len), _dp(pkt_seg), _dp(length), _dp(skip), _dp(seed),
         _dp(out), n, flags, len_hint, _stream(stream)))
+    return out
+
+
+def cksum_mbufs(heads, length=None, skip=None, seed=None, out=None, flags: int = 0,
+                status=None, stream=None):
+    """``in_cksum_skip(heads[i], length[i], skip[i])`` (+ ``seed[i]``) over
+    struct mbuf chains that live in HBM: ``heads`` is an int64 device tensor
+    of first-mbuf device addresses whose m_next / m_data are device addresses
+    too (see :func:`libuinet_amd.workloads.device_mbufs`); optional int32
+    ``length`` / ``skip`` / ``seed`` (None: whole chain / 0 / 0).  ``status``
+    (an int32 device tensor of one element, optional) receives the OR of
+    MBUF_* bits.  One launch of uinet_cksum_mbufs walks and folds."""
+    import torch
+
+    _dev(heads, torch.int64, "heads")
+    for t, nm in ((length, "length"), (skip, "skip"), (seed, "seed"), (status, "status")):
+        _dev(t, torch.int32, nm)
+    n = heads.numel()
+    for t, nm in ((length, "length"), (skip, "skip"), (seed, "seed")):
+        if t is not None and t.numel() != n:
+            raise ValueError(f"{nm} must hold one entry per packet")
+    if status is not None and status.numel() < 1:
+        raise ValueError("status needs one element")
+    out = _out(n, out, heads)
+    _check("uinet_cksum_mbufs", lib().uinet_cksum_mbufs(
+        _dp(heads), _dp(length), _dp(skip), _dp(seed), _dp(out), n, flags, _dp(status),
+        _stream(stream)))
     return out
 
 

@@ -1420,6 +1420,16 @@ int uinet_cksum_chains32(const void* base, const uint32_t* seg_off, const uint16
                          len_hint, static_cast<hipStream_t>(stream));
 }
 
+int uinet_cksum_mbufs(const struct mbuf* const* heads, const int32_t* len, const int32_t* skip,
+                      const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                      uint32_t* status, void* stream) {
+  if (n == 0) return UINET_CKSUM_OK;
+  if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
+  if (!heads || !out) return UINET_CKSUM_EINVAL;
+  return launch_mbufs(reinterpret_cast<const uint64_t*>(heads), len, skip, seed, out, n, flags,
+                      status, static_cast<hipStream_t>(stream));
+}
+
 // ---- host-mbuf batch API ------------------------------------------------------
 
 int in_cksum_skip_batch(struct mbuf* const* m, const int* len, const int* skip,

@@ -112,6 +112,19 @@ int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* 
                       uint32_t* seg_len, uint32_t* pkt_seg, uint32_t* len_out, uint32_t* skip_out,
                       uint32_t* seed_out, uint32_t* status, hipStream_t stream);
 
+// The fused mbuf walk + fold (cksum_mbufs.hip).  launch_mbufs: chains in
+// device memory (uinet_cksum_mbufs; status: UINET_CKSUM_MBUF_* bits).
+// launch_mbufs_xlate: chains and bytes in registered host memory read through
+// the region table (status[0]: kWalkUnmapped / kWalkFallback -- the host then
+// redoes the batch; `pseudo`: the first mbuf must hold skip).
+int launch_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* skip,
+                 const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
+                 uint32_t* status, hipStream_t stream);
+int launch_mbufs_xlate(const uint64_t* heads, const int32_t* len, const int32_t* skip,
+                       const uint32_t* seed, const WalkRegionHost* regions, int nreg, bool pseudo,
+                       uint16_t* out, uint32_t n, uint32_t flags, uint32_t* status,
+                       hipStream_t stream);
+
 // Driver hooks on the device (cksum_hookdev.hip): k_hook_parse writes two jobs
 // per frame (jm / jl / js / jd: 2n entries) and its plan / frame records
 // (hook_plan_bytes / hook_frame_bytes each); k_hook_apply writes the verdicts

@@ -303,6 +303,66 @@ def materialize_device(lay, device="cuda"):
                 bytes=lay["bytes"], layout=lay)
 
 
+# ---- the same chains as struct mbufs in HBM (uinet_cksum_mbufs) ----------------
+
+def device_mbufs(arena, seg_off, seg_len, pkt_seg, shuffle: int | None = None):
+    """struct mbuf chains in HBM over a device arena, one 256-B record
+    (MSIZE, sys/sys/param.h:159) per segment, the way MbufChains lays them out
+    on the host: m_next (offset 0) and m_data (16) are DEVICE addresses, m_len
+    (24) the segment length, M_PKTHDR in the first mbuf's m_flags (28).
+    Records sit in chain order, or -- with ``shuffle`` a seed -- at a random
+    permutation of the slots (a UMA zone's free list hands mbufs out in no
+    particular order).  Returns dict(mbufs=int64 tensor (nseg, 32),
+    heads=int64 tensor of the first mbufs' addresses, 0 for an empty chain)."""
+    import torch
+
+    dev = arena.device
+    seg_off = torch.as_tensor(seg_off).to(dev, torch.int64)
+    seg_len = torch.as_tensor(seg_len).to(dev, torch.int64)
+    pkt_seg = torch.as_tensor(pkt_seg).to(dev, torch.int64)
+    nseg, n = seg_off.numel(), pkt_seg.numel() - 1
+    mb = torch.zeros((max(nseg, 1), 32), dtype=torch.int64, device=dev)
+    if shuffle is None:
+        slot = torch.arange(nseg, dtype=torch.int64, device=dev)
+    else:
+        g = torch.Generator(device="cpu").manual_seed(int(shuffle))
+        slot = torch.randperm(nseg, generator=g).to(dev)
+    addr = mb.data_ptr() + 256 * slot
+    nonempty = pkt_seg[1:] > pkt_seg[:-1]
+    first = pkt_seg[:-1][nonempty]
+    last = pkt_seg[1:][nonempty] - 1
+    nxt = torch.zeros(nseg, dtype=torch.int64, device=dev)
+    if nseg > 1:
+        nxt[:-1] = addr[1:]
+    nxt[last] = 0
+    if nseg:
+        mb[slot, 0] = nxt
+        mb[slot, 2] = arena.data_ptr() + seg_off
+        flags = torch.zeros(nseg, dtype=torch.int64, device=dev)
+        flags[first] = 0x2  # M_PKTHDR
+        mb[slot, 3] = (seg_len & 0xFFFFFFFF) | (flags << 32)
+    heads = torch.zeros(n, dtype=torch.int64, device=dev)
+    heads[nonempty] = addr[first]
+    return dict(mbufs=mb, heads=heads)
+
+
+def mbufs_walked(seg_len, pkt_seg, lens, skip) -> int:
+    """How many mbufs in_cksum_skip(m, len, skip) reads (in_cksum.c:203-229):
+    every mbuf that starts before byte len of its chain (the skip walk reads
+    the ones before `skip` too), when len > skip; none otherwise."""
+    seg_len = np.asarray(seg_len, np.int64)
+    pkt_seg = np.asarray(pkt_seg, np.int64)
+    n = pkt_seg.size - 1
+    seg_pkt = np.repeat(np.arange(n), np.diff(pkt_seg))
+    run = np.cumsum(seg_len) - seg_len
+    pos = run - run[np.minimum(pkt_seg[:-1], max(run.size - 1, 0))][seg_pkt]
+    lens = np.asarray(lens, np.int64) if lens is not None else np.full(n, np.iinfo(np.int64).max)
+    skip = np.zeros(n, np.int64) if skip is None else np.broadcast_to(np.asarray(skip, np.int64), (n,))
+    lens = np.broadcast_to(lens, (n,))
+    want = (lens > skip)[seg_pkt]
+    return int(np.count_nonzero(want & (pos < lens[seg_pkt])))
+
+
 def clipped_segments(seg_off, seg_len, pkt_seg, lens, skip):
     """Per segment, the arena bytes [start, end) that in_cksum_skip(m, len,
     skip) sums (in_cksum.c:203-229: len counts from the chain start), for the
