@@ -145,43 +145,28 @@ int uinet_cksum_device_ok(void);
 
 /* Performance knobs (process-wide; they never change results):
  *   "blocks_per_cu"   grid-stride launch width, 0 = per-kernel default
- *   "chains_pass"     64-chunk passes per pipelined batch in the chain
- *                     kernel: 2 (default) or 4
  *   "chains_long"     chain segments of at least this many 16-B chunks are
  *                     streamed wave-wide; 0 = never, else >= 16 (default 128)
- *   "chains_tile"     packets per wave in the chain kernel: 0 = auto, 8, 32
- *   "xcd_remap"       span kernels: give each XCD a contiguous band of
- *                     packets (1, default) or plain block order (0)
- *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
- *                     1..64 (default min(16, hardware threads))
- *   "spans_pipe"      span kernel family (span and strided APIs):
- *                     1 (default) persistent waves with mask-free whole
- *                     chunks and the per-packet work shared across the wave
- *                     (k_spans_lean at 32 / 64 lanes per packet, k_spans_quad
- *                     at 4); 0 = one packet per lane group, one-shot grid
- *   "spans_geo"       span kernels: force the lanes-per-packet G and loads
- *                     per lane U as G * 16 + U (one of 4x1, 4x2, 8x1, 8x2,
- *                     16x3, 32x3, 64x2, 64x3, 64x9); 0 = picked from len_hint
- *   "walk_prefetch"   host-mbuf batch walk: 0 = no prefetch, 1 = prefetch
- *                     mbuf headers a few packets ahead (default)
- *   "host_pin"        host pool helpers pinned to CPUs of the process mask
- *                     (1) or floating (0, default)
- *   "multi_gather"    uinet_cksum_spans_multi: 0 = one RCCL gather when it
- *                     applies (default), 1 = always peer copies
- *   "walk_device"     host-mbuf batches (2c, 2d) whose mbufs AND bytes lie in
- *                     registered memory: 1 (default) the GPU walks the chains,
- *                     the host only writes the jobs; 0 the host walks them
  *   "chains_wide"     chain API: 0 (default) one wave per packet when
  *                     len_hint (mean segment bytes) is 4096-9216, else the
  *                     tile kernel; 1 = always the tile kernel, 2 = always
  *                     one wave per packet
+ *   "xcd_remap"       span kernels: give each XCD a contiguous band of
+ *                     packets (1, default) or plain block order (0)
+ *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
+ *                     1..64 (default min(16, hardware threads))
+ *   "walk_device"     host-mbuf batches (2c, 2d) whose mbufs AND bytes lie in
+ *                     registered memory: 1 (default) the GPU walks the chains
+ *                     and folds their bytes in one launch, the host only writes
+ *                     the jobs; 2 the same as a walk into a segment list, then
+ *                     the chain kernel; 0 the host walks them
+ *   "multi_gather"    uinet_cksum_spans_multi: 0 = one RCCL gather when it
+ *                     applies (default), 1 = always peer copies
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU,
- * UINET_CKSUM_CHAINS_PASS, UINET_CKSUM_CHAINS_LONG, UINET_CKSUM_CHAINS_TILE,
- * UINET_CKSUM_XCD_REMAP, UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_PF,
- * UINET_CKSUM_SPANS_GEO, UINET_CKSUM_SPANS_PIPE, UINET_CKSUM_HOST_PIN,
- * UINET_CKSUM_MULTI_GATHER, UINET_CKSUM_WALK_DEVICE and
- * UINET_CKSUM_CHAINS_WIDE set the initial values. */
+ * UINET_CKSUM_CHAINS_LONG, UINET_CKSUM_CHAINS_WIDE, UINET_CKSUM_XCD_REMAP,
+ * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_DEVICE and
+ * UINET_CKSUM_MULTI_GATHER set the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
 /* ------------------------------------------------------------------------ */

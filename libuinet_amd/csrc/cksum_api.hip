@@ -64,9 +64,8 @@ void note_kernel(const void* host_stub) { t_last_kernel = host_stub; }
 // launch, so each knob is a relaxed atomic and a launch reads one snapshot
 // (tuning()).  The environment seeds them through the same validation.
 struct TuningLive {
-  std::atomic<int> blocks_per_cu{0}, chains_pass{2}, host_threads{8}, chains_long{128},
-      chains_tile{0}, xcd_remap{1}, walk_prefetch{1}, spans_geo{0}, spans_pipe{1},
-      host_pin{0}, multi_gather{0}, walk_device{1}, chains_wide{0};
+  std::atomic<int> blocks_per_cu{0}, host_threads{8}, chains_long{128}, xcd_remap{1},
+      multi_gather{0}, walk_device{1}, chains_wide{0};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -77,19 +76,12 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
   };
   static const Knob knobs[] = {
       {"blocks_per_cu", &TuningLive::blocks_per_cu, [](int v) { return v >= 0 && v <= 4096; }},
-      {"chains_pass", &TuningLive::chains_pass, [](int v) { return v == 2 || v == 4; }},
       {"chains_long", &TuningLive::chains_long,
        [](int v) { return v == 0 || (v >= 16 && v <= (1 << 24)); }},
-      {"chains_tile", &TuningLive::chains_tile,
-       [](int v) { return v == 0 || v == 8 || v == 32; }},
       {"xcd_remap", &TuningLive::xcd_remap, [](int v) { return v == 0 || v == 1; }},
       {"host_threads", &TuningLive::host_threads, [](int v) { return v >= 1 && v <= 64; }},
-      {"spans_geo", &TuningLive::spans_geo, [](int v) { return v == 0 || span_geometry_ok(v); }},
-      {"spans_pipe", &TuningLive::spans_pipe, [](int v) { return v == 0 || v == 1; }},
-      {"walk_prefetch", &TuningLive::walk_prefetch, [](int v) { return v == 0 || v == 1; }},
-      {"host_pin", &TuningLive::host_pin, [](int v) { return v == 0 || v == 1; }},
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
-      {"walk_device", &TuningLive::walk_device, [](int v) { return v == 0 || v == 1; }},
+      {"walk_device", &TuningLive::walk_device, [](int v) { return v >= 0 && v <= 2; }},
       {"chains_wide", &TuningLive::chains_wide, [](int v) { return v >= 0 && v <= 2; }},
   };
   for (const Knob& k : knobs)
@@ -103,13 +95,10 @@ static TuningLive& tuning_live() {
     const unsigned hw = std::thread::hardware_concurrency();
     x->host_threads = (int)std::min(16u, hw ? hw : 1u);
     static const char* const env[][2] = {
-        {"UINET_CKSUM_BLOCKS_PER_CU", "blocks_per_cu"}, {"UINET_CKSUM_CHAINS_PASS", "chains_pass"},
-        {"UINET_CKSUM_CHAINS_LONG", "chains_long"},     {"UINET_CKSUM_CHAINS_TILE", "chains_tile"},
+        {"UINET_CKSUM_BLOCKS_PER_CU", "blocks_per_cu"}, {"UINET_CKSUM_CHAINS_LONG", "chains_long"},
         {"UINET_CKSUM_XCD_REMAP", "xcd_remap"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
-        {"UINET_CKSUM_WALK_PF", "walk_prefetch"},       {"UINET_CKSUM_SPANS_GEO", "spans_geo"},
-        {"UINET_CKSUM_SPANS_PIPE", "spans_pipe"},
-        {"UINET_CKSUM_HOST_PIN", "host_pin"},          {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},
-        {"UINET_CKSUM_WALK_DEVICE", "walk_device"},     {"UINET_CKSUM_CHAINS_WIDE", "chains_wide"},
+        {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},   {"UINET_CKSUM_WALK_DEVICE", "walk_device"},
+        {"UINET_CKSUM_CHAINS_WIDE", "chains_wide"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -129,15 +118,9 @@ Tuning tuning() {
   const auto ld = [](const std::atomic<int>& a) { return a.load(std::memory_order_relaxed); };
   Tuning x;
   x.blocks_per_cu = ld(t.blocks_per_cu);
-  x.chains_pass = ld(t.chains_pass);
   x.host_threads = ld(t.host_threads);
   x.chains_long = ld(t.chains_long);
-  x.chains_tile = ld(t.chains_tile);
   x.xcd_remap = ld(t.xcd_remap);
-  x.walk_prefetch = ld(t.walk_prefetch);
-  x.spans_geo = ld(t.spans_geo);
-  x.spans_pipe = ld(t.spans_pipe);
-  x.host_pin = ld(t.host_pin);
   x.multi_gather = ld(t.multi_gather);
   x.walk_device = ld(t.walk_device);
   x.chains_wide = ld(t.chains_wide);
@@ -544,14 +527,13 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
   // chunks per pipeline group: one per thread (one pool pass each; 2-64 per
   // thread lost in every A/B, profiles/r04/pruned/knobs.diff)
   const int group = std::max(1, threads);
-  const bool pin = tuning().host_pin != 0;
   size_t ring = 0;  // next free byte of the descriptor ring in c.h_buf
   uint64_t total = 0;
   size_t np_all = 0;
   for (int g0 = 0; g0 < nch; g0 += group) {
     const int g1 = std::min(nch, g0 + group);
     clk::time_point ta = trace ? clk::now() : clk::time_point();
-    pool.run(g1 - g0, threads, [&](int jj) { walk_chunk(g0 + jj); }, pin);
+    pool.run(g1 - g0, threads, [&](int jj) { walk_chunk(g0 + jj); });
     clk::time_point tb = trace ? clk::now() : clk::time_point();
     if (trace) t_walk += std::chrono::duration<double, std::milli>(tb - ta).count();
 
@@ -618,7 +600,7 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
         ps[i - i0] = C.first_piece + B.pk_first[(size_t)i];
         sd[i - i0] = B.seed[(size_t)i];
       }
-    }, pin);
+    });
     ps[ng] = (uint32_t)np;
     for (int j = g0; j < g1; j++) bad |= B.chunks[(size_t)j].unmapped;
     if (trace) t_desc += std::chrono::duration<double, std::milli>(clk::now() - tb).count();
@@ -794,15 +776,17 @@ bool heads_registered(int n, const HeadAt& head_at) {
 // job(i) -> Job (the in_cksum_skip form; len and skip as the caller gave
 // them).  Returns kFallback (nothing delivered) when the batch must take the
 // host walk.  Called with g_reg_mu held (shared) and at least one region.
-template <typename JobFn>
+template <typename HeadFn, typename JobFn>
 int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32_t flags,
-                      WalkKind kind, bool seeded, const JobFn& job, uint16_t* out16,
-                      unsigned* out32, bool trace) {
+                      WalkKind kind, bool seeded, const HeadFn& head, const JobFn& job,
+                      uint16_t* out16, unsigned* out32, bool trace) {
   using clk = std::chrono::steady_clock;
   const clk::time_point t0 = trace ? clk::now() : clk::time_point();
   const size_t nreg_all = g_regions.size();
   if (nreg_all == 0 || nreg_all > (size_t)kWalkRegionsMax) return kFallback;
-  if (!heads_registered(n, [&](int i) { return job(i).m; })) return kFallback;
+  // head(i) is side-effect free (job(i) of a hook parses the frame)
+  if (!heads_registered(n, [&](int i) { return head(i).m; })) return kFallback;
+  const bool fused = tuning().walk_device == 1;
   uint32_t K = c.walk_k ? c.walk_k : 4;
   const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const size_t N = (size_t)n;
@@ -811,8 +795,8 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
   const size_t h_len = a16(8 * N), h_skip = h_len + a16(4 * N), h_seed = h_skip + a16(4 * N);
   const size_t h_reg = h_seed + (seeded ? a16(4 * N) : 0);
   const size_t h_st = h_reg + a16(sizeof(WalkRegionHost) * nreg_all), h_end = h_st + 16;
-  // HBM: status u32[4] | the walk's work area
-  int rc = ctx_reserve(c, h_end, N, 16 + walk_work(N, K).end);
+  // HBM: status u32[4] | the two-pass walk's work area
+  int rc = ctx_reserve(c, h_end, N, fused ? 16 : 16 + walk_work(N, K).end);
   if (rc) return rc;
   uint8_t* h = c.h_buf;
   uint64_t* heads = reinterpret_cast<uint64_t*>(h);
@@ -831,7 +815,7 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
       js[i] = J.skip;
       if (seeded) jd[i] = J.seed;
     }
-  }, tuning().host_pin != 0);
+  });
   size_t nreg = 0;
   uint64_t lo_addr = 0;
   (void)walk_regions(reinterpret_cast<WalkRegionHost*>(h + h_reg), nreg_all, &nreg, &lo_addr);
@@ -844,6 +828,39 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
   if (rc) return rc;
   const uint8_t* dj = static_cast<const uint8_t*>(dh);
   volatile uint32_t* st = reinterpret_cast<volatile uint32_t*>(h + h_st);
+  if (fused) {
+    // one launch walks the chains and folds their bytes (cksum_mbufs.hip),
+    // reading jobs, mbuf headers and packet bytes in place over PCIe
+    uint32_t* dstatus = reinterpret_cast<uint32_t*>(c.d_buf);
+    rc = record_hip(hipMemsetAsync(dstatus, 0, 8, c.stream));
+    if (!rc)
+      rc = launch_mbufs_xlate(reinterpret_cast<const uint64_t*>(dj),
+                              reinterpret_cast<const int32_t*>(dj + h_len),
+                              reinterpret_cast<const int32_t*>(dj + h_skip),
+                              seeded ? reinterpret_cast<const uint32_t*>(dj + h_seed) : nullptr,
+                              reinterpret_cast<const WalkRegionHost*>(dj + h_reg), (int)nreg,
+                              kind == kWalkPseudo, static_cast<uint16_t*>(dout), (uint32_t)N,
+                              flags, dstatus, c.stream);
+    if (!rc)
+      rc = record_hip(hipMemcpyAsync(h + h_st, dstatus, 8, hipMemcpyDeviceToHost, c.stream));
+    const int wrc = ctx_wait(c);
+    if (rc) return rc;
+    if (wrc) return wrc;
+    if (st[0]) return kFallback;  // a job the host walk must take
+    for (int i = 0; i < n; i++) {
+      if (out16) out16[i] = c.h_out[i];
+      if (out32) out32[i] = c.h_out[i];
+    }
+    note_device_walk();
+    if (trace)
+      fprintf(stderr,
+              "uinet_cksum host batch: n=%d device walk (fused) | jobs %.3f fold %.3f total "
+              "%.3f ms\n",
+              n, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(clk::now() - t1).count(),
+              std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+    return UINET_CKSUM_OK;
+  }
   for (int attempt = 0; attempt < 2; attempt++) {
     rc = ctx_reserve(c, h_end, N, 16 + walk_work(N, K).end);
     if (rc) return rc;
@@ -896,9 +913,9 @@ struct ChainRef {
 // Walk prefetch.  The walk is bound by misses on mbuf headers
 // (m_next/m_data/m_len share the first line), each dependent on the previous
 // one, so walking one chain after another keeps about one miss in flight per
-// thread.  prefetch_ahead requests headers a few packets ahead (knob
-// "walk_prefetch", env UINET_CKSUM_WALK_PF: 1 default, 0 off).  A lockstep
-// chase of 16 chains (equal on config 3, 3-12 % slower on the offload hooks,
+// thread.  prefetch_ahead requests headers a few packets ahead (the knob that
+// turned it off went in round 6, profiles/r06/pruned/).  A lockstep chase of
+// 16 chains (equal on config 3, 3-12 % slower on the offload hooks,
 // profiles/r01/ab/walk_pf/) was removed in round 4 (profiles/r04/pruned/).
 // Plain software prefetch ahead: packet i+16's head, i+8's second mbuf,
 // i+4's third (each read from a line an earlier step requested).
@@ -950,7 +967,6 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   using clk = std::chrono::steady_clock;
   const clk::time_point t_start = trace ? clk::now() : clk::time_point();
   clk::time_point t_walk, t_place, t_fill, t_launch;
-  const int prefetch = tuning().walk_prefetch;  // 0 off, 1 ahead (default)
 
   // Walk chunk j: every packet as the reference walks it, into the chunk's
   // piece list (pk_first chunk-local).
@@ -964,7 +980,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     C.odd = C.too_big = C.unmapped = false;
     C.w.long_piece = false;
     for (int i = C.i0; i < C.i1; i++) {
-      if (prefetch == 1) {
+      {  // headers a few packets ahead
         if (i + 16 < C.i1) prefetch_ahead(head(i + 16), 0);
         if (i + 8 < C.i1) prefetch_ahead(head(i + 8), 1);
         if (i + 4 < C.i1) prefetch_ahead(head(i + 4), 2);
@@ -997,8 +1013,8 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   if (n > stage_below) {
     std::shared_lock<std::shared_mutex> g(g_reg_mu);
     if (!g_regions.empty() && kind != kWalkNone && tuning().walk_device) {
-      rc = device_walk_batch(c, pool, threads, cs, n, flags, kind, seeded, job, out16, out32,
-                             trace);
+      rc = device_walk_batch(c, pool, threads, cs, n, flags, kind, seeded, head, job, out16,
+                             out32, trace);
       if (rc != kFallback) return rc;
     }
     if (!g_regions.empty()) {
@@ -1015,7 +1031,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   }
 
   // (1) walk
-  pool.run(nch, threads, walk_chunk, tuning().host_pin != 0);
+  pool.run(nch, threads, walk_chunk);
 
   if (trace) t_walk = clk::now();
   // (2) place the chunks
@@ -1070,7 +1086,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
           }
           cur += ((uint64_t)B.bytes[(size_t)i] + 15) & ~uint64_t(15);
         }
-      }, tuning().host_pin != 0);
+      });
       if (stream_copy) {
         const uint64_t b0 = B.chunks[(size_t)g0].pack_base;
         const uint64_t b1 = g1 < nch ? B.chunks[(size_t)g1].pack_base : packed;
@@ -1183,9 +1199,10 @@ int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* 
   const size_t d_jd = d_js + a16(4 * J), d_pl = d_jd + a16(4 * J);
   const size_t d_fr = d_pl + a16(hook_plan_bytes(rx) * N), d_res = d_fr + a16(hook_frame_bytes() * N);
   const size_t d_wa = d_res + a16(2 * J);
-  uint32_t K = c.walk_k ? c.walk_k : 4;
+  const bool fused = tuning().walk_device == 1;
+  uint32_t K = fused ? 0u : c.walk_k ? c.walk_k : 4;
   if ((uint64_t)J * K > 0xffffffffull) return kFallback;  // rows indexed by u32
-  rc = ctx_reserve(c, h_end, N, d_wa + walk_work(J, K).end);
+  rc = ctx_reserve(c, h_end, N, d_wa + (fused ? 0 : walk_work(J, K).end));
   if (rc) return rc;
   uint8_t* h = c.h_buf;
   memcpy(h, mv, 8 * N);
@@ -1199,8 +1216,8 @@ int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* 
   const WalkRegionHost* dregs = reinterpret_cast<const WalkRegionHost*>(dh + h_reg);
   volatile uint32_t* st = reinterpret_cast<volatile uint32_t*>(h + h_st);
   bool parsed = false;
-  for (int attempt = 0; attempt < 2; attempt++) {
-    rc = ctx_reserve(c, h_end, N, d_wa + walk_work(J, K).end);
+  for (int attempt = 0; attempt < (fused ? 1 : 2); attempt++) {
+    rc = ctx_reserve(c, h_end, N, d_wa + (fused ? 0 : walk_work(J, K).end));
     if (rc) return rc;
     uint8_t* d = c.d_buf;
     uint32_t* dstatus = reinterpret_cast<uint32_t*>(d);
@@ -1215,7 +1232,11 @@ int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* 
       rc = launch_hook_parse(rx, reinterpret_cast<const uint64_t*>(dh), (uint32_t)n, l2len,
                              dregs, (int)nreg, jm, jl, js, jd, d + d_pl, d + d_fr, dstatus,
                              c.stream);
-    if (!rc)
+    if (!rc && fused)  // the jobs' chains walked and folded in one launch
+      rc = launch_mbufs_xlate(jm, jl, js, jd, dregs, (int)nreg, false,
+                              reinterpret_cast<uint16_t*>(d + d_res), (uint32_t)J, 0, dstatus,
+                              c.stream);
+    else if (!rc)
       rc = launch_walk_fold(c, jm, jl, js, jd, dregs, (int)nreg, lo, J, K, false, d + d_wa,
                             dstatus, reinterpret_cast<uint16_t*>(d + d_res), 0);
     if (!rc)
@@ -1226,9 +1247,9 @@ int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* 
     if (rc) return rc;
     if (wrc) return wrc;
     if (st[0]) return kFallback;  // the device view could not take a frame
-    const uint32_t longest = st[1];
+    const uint32_t longest = st[1];  // 0 after the fused walk
     const uint32_t k2 = walk_k_for(longest);
-    c.walk_k = k2;
+    if (!fused) c.walk_k = k2;
     if (longest <= K) {  // the apply step ran
       if (status) memcpy(status, h + h_v, N);
       note_device_walk();

@@ -566,8 +566,12 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
     return check_launch();
   }
   // Tile of 32 packets, or 8 when 32 would give fewer than 16 tiles per CU
-  // (5tso, 131 K packets, runs 0.8 % faster at 32: profiles/r01/ab/bpc_s6/tile).
-  const int tile = tn.chains_tile ? tn.chains_tile : (n >= 32u * 4096u ? 32 : 8);
+  // (5tso, 131 K packets, runs 0.8 % faster at 32: profiles/r01/ab/bpc_s6/tile;
+  // the 128 K switch rechecked on mid-size config-3 batches, profiles/r05/r05tile/).
+  // Two 64-chunk passes per batch: four lost on every config
+  // (profiles/r01/ab/chains_pipe/); the chains_pass / chains_tile knobs that
+  // forced other shapes were removed in round 6 (profiles/r06/pruned/).
+  const int tile = n >= 32u * 4096u ? 32 : 8;
   const uint32_t tiles = (n + (uint32_t)tile - 1) / (uint32_t)tile;
   uint64_t blocks = (tiles + kWaves - 1) / kWaves;
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(64);
@@ -576,13 +580,10 @@ int launch_chains_t(const void* base, const OffT* seg_off, const LenT* seg_len,
 #define LF(P, T)                                                                           \
   UINET_LAUNCH((k_chains_pipe<P, T, OffT, LenT>), dim3((int)blocks), dim3(kBlock), 0,   \
                stream, b, seg_off, seg_len, pkt_seg, len, skip, seed, out, n, flags, long_ch)
-  if (tile == 8) {
-    if (tn.chains_pass == 4) LF(4, 8);
-    else LF(2, 8);
-  } else {
-    if (tn.chains_pass == 4) LF(4, 32);
-    else LF(2, 32);
-  }
+  if (tile == 8)
+    LF(2, 8);
+  else
+    LF(2, 32);
 #undef LF
   return check_launch();
 }

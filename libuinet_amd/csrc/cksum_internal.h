@@ -15,27 +15,18 @@ namespace uinet {
 // a snapshot of the live values (relaxed atomics in cksum_api.hip).
 struct Tuning {
   int blocks_per_cu;   // grid-stride width
-  int chains_pass;     // flat chains: 64-chunk passes per pipelined batch, 2 or 4
   int host_threads;    // host-mbuf batch walk/pack threads, 1..64
   int chains_long;     // flat chains: segments of >= this many 16-B chunks stream
                        // wave-wide (0 = never)
-  int chains_tile;     // flat chains: packets per wave tile, 0 = auto, 8, 32
   int chains_wide;     // chains: 0 = a wave per packet (k_chains_wide) when the mean
                        // segment is 4-9 KiB, 1 = never, 2 = always
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
-  int spans_pipe;      // span kernel family: 1 k_spans_lean / k_spans_quad (persistent,
-                       // mask-free whole chunks), 0 one-shot k_spans
-  int spans_geo;       // span kernels: lanes-per-packet G and loads-per-lane U
-                       // as G * 16 + U (0 = picked from the mean length)
-  int walk_prefetch;   // host walk: 0 off, 1 prefetch ahead
-  int host_pin;        // host pool helpers pinned to CPUs 1.. of the process mask (0/1)
   int multi_gather;    // uinet_cksum_spans_multi: 0 RCCL gather when it applies, 1 peer copies
-  int walk_device;     // host-mbuf batches in registered memory: 1 the GPU walks the chains
-                       // (cksum_walk.hip), 0 the host walks them
+  int walk_device;     // host-mbuf batches in registered memory: 1 the GPU walks and folds
+                       // the chains in one launch (cksum_mbufs.hip), 2 walks them into a
+                       // segment list first (cksum_walk.hip), 0 the host walks them
 };
 Tuning tuning();
-// True when G * 16 + U names a compiled span-kernel geometry.
-bool span_geometry_ok(int code);
 
 // Records the HIP error (if any) of the last launch on this thread and maps
 // it to a UINET_CKSUM_* code.

@@ -30,74 +30,7 @@
 namespace uinet {
 namespace {
 
-// Scalar (SMEM) loads of words the kernel never writes: through the constant
-// address space a uniform load becomes an s_load, served by the scalar cache
-// instead of the vector memory pipeline that streams the packet bytes.
-__device__ __forceinline__ uint64_t sload64(const uint64_t* p) {
-  return *(const __attribute__((address_space(4))) uint64_t*)(uintptr_t)p;
-}
-__device__ __forceinline__ uint32_t sload32(const uint32_t* p) {
-  return *(const __attribute__((address_space(4))) uint32_t*)(uintptr_t)p;
-}
-// Span descriptors, wide (u64 offset, u32 length) or packed (u32 offset,
-// u16 length: uinet_cksum_spans32; a u16 comes from the aligned dword that
-// holds it).
-__device__ __forceinline__ uint64_t sload_off(const uint64_t* p) { return sload64(p); }
-__device__ __forceinline__ uint64_t sload_off(const uint32_t* p) { return sload32(p); }
-__device__ __forceinline__ uint32_t sload_len(const uint32_t* p) { return sload32(p); }
-__device__ __forceinline__ uint32_t sload_len(const uint16_t* p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  return (sload32(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)) >> (8 * (a & 2))) & 0xffffu;
-}
-
-// The descriptors of packet p for lane group `gi` of a wave whose kP = 64 / G
-// groups own the consecutive packets p - gi .. p - gi + kP - 1: kP scalar
-// loads of off / len (clamped to n - 1), then a per-lane select.  Without
-// it every group's off[p] / len[p] is a vector load of its own, 2 of the 5
-// vector-memory instructions per wave and packet pair at 1500 B.
-template <int G, typename OffT, typename LenT>
-__device__ __forceinline__ void wave_desc(const OffT* __restrict__ off,
-                                          const LenT* __restrict__ len, uint32_t p, uint32_t n,
-                                          uint64_t& o, uint32_t& l) {
-  constexpr int kP = 64 / G;
-  const uint32_t gi = (threadIdx.x & 63) / G;
-  const uint32_t p0 = __builtin_amdgcn_readfirstlane(p - gi);
-  o = 0;
-  l = 0;
-#pragma unroll
-  for (int k = 0; k < kP; ++k) {
-    const uint32_t q = min(p0 + (uint32_t)k, n - 1);
-    // readfirstlane keeps each value scalar: without it the compiler folds
-    // the select of kP loads back into one per-lane (vector) load of off[p]
-    const uint64_t o64 = sload_off(off + q);
-    const uint64_t ok = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o64 >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)o64);
-    const uint32_t lk = __builtin_amdgcn_readfirstlane(sload_len(len + q));
-    if (gi == (uint32_t)k) {
-      o = ok;
-      l = lk;
-    }
-  }
-}
-
-// One u32 per packet (the seed) for the wave's kP packets, by scalar loads.
-template <int G>
-__device__ __forceinline__ uint32_t wave_u32(const uint32_t* __restrict__ a, uint32_t p,
-                                             uint32_t n) {
-  constexpr int kP = 64 / G;
-  const uint32_t gi = (threadIdx.x & 63) / G;
-  const uint32_t p0 = __builtin_amdgcn_readfirstlane(p - gi);
-  uint32_t r = 0;
-#pragma unroll
-  for (int k = 0; k < kP; ++k) {
-    const uint32_t v = __builtin_amdgcn_readfirstlane(sload32(a + min(p0 + (uint32_t)k, n - 1)));
-    if (gi == (uint32_t)k) r = v;
-  }
-  return r;
-}
-
-template <int G, int U, bool kStrided, bool kSDesc = false, typename OffT = uint64_t,
-          typename LenT = uint32_t>
+template <int G, int U, bool kStrided, typename OffT = uint64_t, typename LenT = uint32_t>
 __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ base,
                                                  const OffT* __restrict__ off,
                                                  const LenT* __restrict__ len,
@@ -118,10 +51,7 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
   const bool live = p < pend;
   uint64_t o = 0;
   uint32_t l = 0;
-  if constexpr (kSDesc && !kStrided) {
-    wave_desc<G>(off, len, p, n, o, l);
-    if (!live) l = 0;
-  } else if (live) {
+  if (live) {
     o = kStrided ? (uint64_t)p * pkt_stride : (uint64_t)off[p];
     l = kStrided ? fixed_len : (uint32_t)len[p];
   }
@@ -138,12 +68,8 @@ __global__ __launch_bounds__(kBlock) void k_spans(const uint8_t* __restrict__ ba
     const uint32_t pc = min(pn, n - 1);
     uint64_t on;
     uint32_t ln;
-    if constexpr (kSDesc && !kStrided) {
-      wave_desc<G>(off, len, pn, n, on, ln);
-    } else {
-      on = kStrided ? (uint64_t)pc * pkt_stride : (uint64_t)off[pc];
-      ln = kStrided ? fixed_len : (uint32_t)len[pc];
-    }
+    on = kStrided ? (uint64_t)pc * pkt_stride : (uint64_t)off[pc];
+    ln = kStrided ? fixed_len : (uint32_t)len[pc];
     // a span of one round folds its 32-bit sum (< U * 2^19) directly
     const uint32_t a0 = l ? sp.sum_lut_first(lut, gl) : 0u;
     uint32_t x =
@@ -195,38 +121,23 @@ int grid_for(uint32_t n, int g, int bpc) {
   return (int)blocks;
 }
 
-// Compiled geometries (G * 16 + U); the "spans_geo" knob forces one for A/B.
-// 16 x 6 and 8 x 12 (the 96 chunks of 32 x 3 with twice / four times the
-// bytes in flight per lane) needed 82 / 132 VGPRs and ran 2-3 % slower on
-// config 2 (profiles/r02/ab_geo/), so they are not built.
+// The geometries k_spans runs (G * 16 + U): 8 and 16 lanes per packet, and 4
+// x 2 for the strided form of unaligned small packets.  32 and 64 lanes run
+// k_spans_lean and 4 x 1 / 4 x 2 spans k_spans_quad (cksum_spans.hip).  16 x 6
+// and 8 x 12 (the 96 chunks of 32 x 3 with twice / four times the bytes in
+// flight per lane) needed 82 / 132 VGPRs and ran 2-3 % slower on config 2
+// (profiles/r02/ab_geo/), so they are not built; the spans_geo / spans_pipe
+// knobs that forced other geometries and a one-shot k_spans at 32 / 64 lanes
+// were removed in round 6 (profiles/r06/pruned/).
 #define UINET_DISPATCH_GEOMETRY(GEO, LAUNCH)          \
   switch ((GEO).g * 16 + (GEO).u) {                   \
-    case 4 * 16 + 1: LAUNCH(4, 1); break;             \
     case 4 * 16 + 2: LAUNCH(4, 2); break;             \
     case 8 * 16 + 1: LAUNCH(8, 1); break;             \
     case 8 * 16 + 2: LAUNCH(8, 2); break;             \
-    case 16 * 16 + 3: LAUNCH(16, 3); break;           \
-    case 32 * 16 + 3: LAUNCH(32, 3); break;           \
-    case 64 * 16 + 2: LAUNCH(64, 2); break;           \
-    default: LAUNCH(64, 3); break;                    \
+    default: LAUNCH(16, 3); break;                    \
   }
 
 }  // namespace
-
-bool span_geometry_ok(int code) {
-  switch (code) {
-    case 4 * 16 + 1: case 4 * 16 + 2: case 8 * 16 + 1: case 8 * 16 + 2: case 16 * 16 + 3:
-    case 32 * 16 + 3: case 64 * 16 + 2: case 64 * 16 + 3: case 64 * 16 + 9:
-      return true;
-    default:
-      return false;
-  }
-}
-
-static Geometry geometry_override(Geometry g) {
-  const int v = tuning().spans_geo;
-  return v ? Geometry{v / 16, v % 16} : g;
-}
 
 // Blocks per CU.  Measured on MI355X by interleaved A/B (config 2,
 // profiles/r01/ab/): the span kernel peaks at 256 (2 packets per group --
@@ -239,46 +150,29 @@ int blocks_per_cu(int dflt) {
   return v > 0 ? v : dflt;
 }
 
-// spans_pipe selects the span kernel family for G >= 32 (knob "spans_pipe",
-// UINET_CKSUM_SPANS_PIPE):
-//   1 (default) k_spans_lean (cksum_spans.hip): persistent waves, scalar
-//     descriptors, mask-free whole chunks -- 23 VALU instructions per KiB,
-//     no power-ramp dip in the driver's window (profiles/r03/r03d/); at 4
-//     lanes per packet (mean length <= 64 B) k_spans_quad;
-//   0 k_spans: one packet per lane group, one-shot grid.
-// Geometries of 8 and 16 lanes, and 64 x 2 (the spans_geo override), take
-// k_spans under both.  (2 was round 2's k_spans_pp, removed in round 3.)
-// Packed descriptors (uinet_cksum_spans32) take the same kernels.
+// The span kernel family by geometry: 4 lanes per packet (mean length <= 64
+// B) k_spans_quad; 32 and 64 lanes k_spans_lean (cksum_spans.hip): persistent
+// waves, scalar descriptors, mask-free whole chunks -- 23 VALU instructions
+// per KiB, no power-ramp dip in the driver's window (profiles/r03/r03d/);
+// 8 and 16 lanes k_spans.  Packed descriptors (uinet_cksum_spans32) take the
+// same kernels.
 template <typename OffT, typename LenT>
 static int launch_spans_t(const void* base, const OffT* off, const LenT* len,
                           const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                           uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
-  const Geometry geo = geometry_override(pick_geometry(len_hint));
-  const int pipe = tuning().spans_pipe;
-  // Scalar descriptors for G >= 32: a wave's 1-2 packets' off / len come from
-  // s_loads, and the grid drops to one packet per group (512 blocks per CU at
-  // 1 M x 1500 B).  Interleaved A/B, config 2 (profiles/r02/ab_sdesc/): vector
-  // descriptors at 256 / CU 0.2192 ms, scalar at 256 / CU 0.2167, scalar at
-  // 512 / CU 0.2086 (+5.1 %), 4096 / CU 0.2095.  (The vector-descriptor form
-  // was the knob spans_sdesc = 0 until round 4: profiles/r04/pruned/.)
-  if (pipe == 1 && geo.g == 4)
+  const Geometry geo = pick_geometry(len_hint);
+  if (geo.g == 4)
     return launch_spans_quad(base, off, len, seed, parity, out, n, flags, geo.u, false, 0, 0,
                              blocks_per_cu(128), stream);
-  const bool sdesc = geo.g >= 32;
-  if (sdesc && pipe == 1 && (geo.u == 3 || geo.u == 9))
+  if (geo.g >= 32)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, geo.u, false, 0,
                              0, tuning().blocks_per_cu, stream);
-  const int grid = grid_for(n, geo.g, sdesc ? 512 : 256);
+  const int grid = grid_for(n, geo.g, 256);
 #define L(G, U)                                                                          \
-  if (sdesc && (G) >= 32)                                                                \
-    UINET_LAUNCH((k_spans<G, U, false, true, OffT, LenT>), dim3(grid), dim3(kBlock), \
-                       0, stream, static_cast<const uint8_t*>(base), off, len, seed, parity, \
-                       0ull, 0u, out, n, flags, (uint32_t)tuning().xcd_remap);           \
-  else                                                                                   \
-    UINET_LAUNCH((k_spans<G, U, false, false, OffT, LenT>), dim3(grid), dim3(kBlock), \
-                       0, stream, static_cast<const uint8_t*>(base), off, len, seed, parity, \
-                       0ull, 0u, out, n, flags, (uint32_t)tuning().xcd_remap)
+  UINET_LAUNCH((k_spans<G, U, false, OffT, LenT>), dim3(grid), dim3(kBlock), 0, stream,  \
+               static_cast<const uint8_t*>(base), off, len, seed, parity, 0ull, 0u, out, n,   \
+               flags, (uint32_t)tuning().xcd_remap)
   UINET_DISPATCH_GEOMETRY(geo, L)
 #undef L
   return check_launch();
@@ -302,24 +196,21 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   Geometry geo = pick_geometry(len);
   // 16-B aligned packets of at most 64 B hold at most 4 chunks: one per lane
   if (len <= 64 && ((reinterpret_cast<uintptr_t>(base) | pkt_stride) & 15) == 0) geo = {4, 1};
-  geo = geometry_override(geo);
-  const int pipe = tuning().spans_pipe;
   // small packets laid (nearly) back to back and off 16-B alignment: one dense
   // run of chunks per wave, 5 % faster than k_spans<4, 2> on 2su; aligned
   // ones stay on k_spans_quad<1>, 14 % faster than it (profiles/r03/r03s2m/)
-  if (pipe == 1 && !tuning().spans_geo && len <= 256 &&
-      ((reinterpret_cast<uintptr_t>(base) | pkt_stride) & 15) != 0) {
+  if (len <= 256 && ((reinterpret_cast<uintptr_t>(base) | pkt_stride) & 15) != 0) {
     const int rc = launch_strided_dense(base, pkt_stride, len, seed, out, n, flags,
                                         blocks_per_cu(128), stream);
     if (rc != 1) return rc;
   }
   // k_spans_quad for 16-B aligned packets of <= 64 B (one chunk per lane);
   // unaligned ones run k_spans<4, 2>, 5 % faster there (profiles/r03/r03p/)
-  if (pipe == 1 && geo.g == 4 && geo.u == 1)
+  if (geo.g == 4 && geo.u == 1)
     return launch_spans_quad<uint64_t, uint32_t>(base, nullptr, nullptr, seed, nullptr, out, n,
                                                  flags, 1, true, pkt_stride, len,
                                                  blocks_per_cu(128), stream);
-  if (geo.g >= 32 && pipe == 1 && (geo.u == 3 || geo.u == 9))
+  if (geo.g >= 32)
     return launch_spans_lean<uint64_t, uint32_t>(base, nullptr, nullptr, seed, nullptr, out, n,
                                                  flags, geo.g, geo.u, true, pkt_stride, len,
                                                  tuning().blocks_per_cu, stream);
@@ -327,7 +218,7 @@ int launch_strided(const void* base, uint64_t pkt_stride, uint32_t len, const ui
   // loop (64-B packets: 256 per CU 4.88 vs unbounded 3.96 TB/s, profiles/r01/small/)
   const int grid = grid_for(n, geo.g, len <= 96 ? 256 : 4096);
 #define L(G, U)                                                                        \
-  UINET_LAUNCH((k_spans<G, U, true, false, uint64_t, uint32_t>), dim3(grid),      \
+  UINET_LAUNCH((k_spans<G, U, true, uint64_t, uint32_t>), dim3(grid),             \
                      dim3(kBlock), 0, stream,                                          \
                      static_cast<const uint8_t*>(base), nullptr, nullptr, seed, nullptr, \
                      pkt_stride, len, out, n, flags, (uint32_t)tuning().xcd_remap)

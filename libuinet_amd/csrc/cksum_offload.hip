@@ -87,8 +87,7 @@ void for_chunks(int n, F&& f) {
   int cs = (n + threads * 4 - 1) / (threads * 4);
   if (cs < 1024) cs = 1024;
   const int nch = (n + cs - 1) / cs;
-  host_pool().run(nch, threads, [&](int j) { f(j * cs, j * cs + cs < n ? j * cs + cs : n); },
-                  tuning().host_pin != 0);
+  host_pool().run(nch, threads, [&](int j) { f(j * cs, j * cs + cs < n ? j * cs + cs : n); });
 }
 
 // Packet k of a hook's batch owns jobs 2k (IP header) and 2k + 1 (TCP / UDP);

@@ -37,11 +37,10 @@ inline thread_local uint64_t t_pool_helper_ns = 0;
 class HostPool {
  public:
   // fn(j) for every j in [0, jobs), on at most `threads` threads (the caller
-  // is one of them).  Returns when every job has finished.  `pin`: helper k
-  // runs on CPU k + 1 of the process's affinity mask at that time (the caller,
-  // the application's thread, is left alone), the way the reference's timing
-  // harness pins its threads; unpinned helpers float (knob "host_pin").
-  void run(int jobs, int threads, const std::function<void(int)>& fn, bool pin = false) {
+  // is one of them).  Returns when every job has finished.  Helpers float over
+  // the process's CPUs (pinning them, the knob host_pin until round 6, never
+  // won: profiles/r06/pruned/).
+  void run(int jobs, int threads, const std::function<void(int)>& fn) {
     if (threads <= 1 || jobs <= 1 || !busy_.try_lock()) {
       for (int j = 0; j < jobs; j++) fn(j);
       return;
@@ -51,7 +50,6 @@ class HostPool {
     {
       std::lock_guard<std::mutex> g(mu_);
       fn_ = &fn;
-      pin_ = pin;
       jobs_ = jobs;
       next_.store(0, std::memory_order_relaxed);
       helpers_ = threads - 1;
@@ -80,31 +78,12 @@ class HostPool {
   }
   void loop(int id) {
     uint64_t seen = 0;
-    bool pinned = false;
-    cpu_set_t all;
-    const bool have_all = sched_getaffinity(0, sizeof(all), &all) == 0;
     for (;;) {
-      bool pin;
       {
         std::unique_lock<std::mutex> g(mu_);
         cv_.wait(g, [&] { return gen_ != seen; });
         seen = gen_;
         if (id >= helpers_) continue;  // not part of this run
-        pin = pin_;
-      }
-      if (pin != pinned && have_all) {
-        cpu_set_t set = all;  // unpinned: the whole mask the process started with
-        if (pin) {
-          // the (id + 1)-th CPU of the mask, counting round
-          const int cnt = CPU_COUNT(&all), want = cnt ? (id + 1) % cnt : 0;
-          CPU_ZERO(&set);
-          for (int c = 0, k = 0; c < CPU_SETSIZE; c++)
-            if (CPU_ISSET(c, &all) && k++ == want) {
-              CPU_SET(c, &set);
-              break;
-            }
-        }
-        if (pthread_setaffinity_np(pthread_self(), sizeof(set), &set) == 0) pinned = pin;
       }
       // this helper's CPU time for the run, including what helpers of runs
       // it made itself spent (a multi-device shard's own walk pool)
@@ -125,7 +104,6 @@ class HostPool {
   std::atomic<int> next_{0};
   int jobs_ = 0, helpers_ = 0, pending_ = 0;
   uint64_t helper_ns_ = 0;  // helpers' CPU time in the current run (under mu_)
-  bool pin_ = false;
   uint64_t gen_ = 0;
 };
 

@@ -1,7 +1,6 @@
 // Stress test of libuinet_amd/csrc/host_pool.h (host-only, no HIP): several
 // caller threads run batches concurrently with varying job and thread
-// counts, helpers pinned in some batches and not in others; every job must
-// run exactly once per batch.
+// counts; every job must run exactly once per batch.
 #include <atomic>
 #include <cstdio>
 #include <thread>
@@ -16,7 +15,7 @@ int main() {
       const int jobs = 1 + (it * 7 + t) % 37, threads = 1 + (it + t) % 9;
       std::vector<std::atomic<int>> hit(jobs);
       for (auto& h : hit) h = 0;
-      uinet::host_pool().run(jobs, threads, [&](int j) { hit[j]++; }, (it / 3 + t) % 2 == 0);
+      uinet::host_pool().run(jobs, threads, [&](int j) { hit[j]++; });
       for (auto& h : hit) bad += h.load() != 1;
     }
   };

@@ -15,8 +15,11 @@ Engine paths per workload:
               (nothing registered)
   zero_copy   the packet bytes are registered; the host walks the chains and
               writes descriptors, the GPU reads the bytes in place over PCIe
-  dev_walk    bytes AND mbufs registered; the GPU walks the chains itself
-              (csrc/cksum_walk.hip) -- the host only writes the jobs
+  dev_walk    bytes AND mbufs registered; the GPU walks the chains and folds
+              their bytes in one launch (csrc/cksum_mbufs.hip) -- the host only
+              writes the jobs
+  dev_walk2   the same, walked into a segment list (csrc/cksum_walk.hip) and
+              folded by the chain kernel (knob walk_device 2)
 
 Workloads: c2 (1,048,576 x 1500-B packets, one mbuf each), c3 (262,144
 config-3 chains of 1..256-B mbufs, skip 20), the RX and TX offload hooks on
@@ -99,15 +102,20 @@ PATHS = ("staged", "zero_copy", "dev_walk")
 
 def run_paths(name, n, nbytes, fn, bytes_bufs, mbuf_bufs, threads, reps, check, res):
     """Every engine path x host_threads for one workload; check(out) -> bool."""
-    paths = (("staged", []), ("zero_copy", bytes_bufs), ("dev_walk", bytes_bufs + mbuf_bufs))
+    paths = (("staged", []), ("zero_copy", bytes_bufs), ("dev_walk", bytes_bufs + mbuf_bufs),
+             ("dev_walk2", bytes_bufs + mbuf_bufs))
     for path, bufs in paths:
         if path not in PATHS:
             continue
         for t in threads:
             u.set_tuning("host_threads", t)
+            # dev_walk: the fused walk + fold (walk_device 1); dev_walk2: the
+            # walk into a segment list, then the chain kernel (walk_device 2)
+            u.set_tuning("walk_device", 2 if path == "dev_walk2" else 1)
             with Regs(bufs):
                 fn()  # warm: staging buffers, pool threads, walk row size
                 e, out = meter(fn, reps)
+            u.set_tuning("walk_device", 1)
             e = per_k(e, n, nbytes)
             e["bit_identical"] = bool(check(out))
             key = f"{name}/{path}/{t}t"

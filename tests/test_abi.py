@@ -170,20 +170,18 @@ def test_set_tuning_validation():
     """uinet_cksum_set_tuning accepts each documented knob's range and rejects
     unknown keys and out-of-range values (no device needed)."""
     L = u.lib()
-    ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_pass", 4), ("chains_long", 0),
-          ("chains_long", 16), ("chains_tile", 8), ("xcd_remap", 0), ("host_threads", 64),
-          ("walk_prefetch", 0), ("spans_geo", 0), ("spans_geo", 32 * 16 + 3), ("spans_geo", 64 * 16 + 9),
-          ("host_pin", 1), ("multi_gather", 1), ("spans_pipe", 0), ("spans_pipe", 1),
-          ("walk_device", 0), ("walk_device", 1)]
+    ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_long", 0),
+          ("chains_long", 16), ("xcd_remap", 0), ("host_threads", 64), ("multi_gather", 1),
+          ("walk_device", 0), ("walk_device", 1), ("walk_device", 2), ("chains_wide", 2)]
     # chains_variant, spans_lut, spans_contig and spans_pipe 2 (k_spans_pp)
     # were removed in round 3; spans_sdesc, host_group and walk_prefetch 2 in
-    # round 4
-    bad = [("blocks_per_cu", -1), ("chains_pass", 3), ("chains_pass", 8), ("chains_long", 15),
-           ("chains_tile", 64), ("xcd_remap", 2), ("host_threads", 0), ("walk_prefetch", 2),
-           ("spans_geo", 16 * 16 + 6), ("spans_geo", 5), ("spans_sdesc", 0), ("host_group", 1),
-           ("chains_sweep", 2),
-           ("host_pin", 2), ("multi_gather", 2), ("spans_pipe", 2), ("spans_pipe", 3), ("chains_variant", 0),
-           ("spans_lut", 1), ("spans_contig", 0), ("walk_device", 2), ("walk_device", -1),
+    # round 4; spans_pipe, spans_geo, chains_pass, chains_tile, host_pin and
+    # walk_prefetch in round 6 (profiles/r06/pruned/)
+    bad = [("blocks_per_cu", -1), ("chains_long", 15), ("xcd_remap", 2), ("host_threads", 0),
+           ("spans_sdesc", 0), ("host_group", 1), ("chains_sweep", 2), ("multi_gather", 2),
+           ("chains_variant", 0), ("spans_lut", 1), ("spans_contig", 0), ("walk_device", 3),
+           ("walk_device", -1), ("chains_wide", 3), ("spans_pipe", 1), ("spans_geo", 0),
+           ("chains_pass", 2), ("chains_tile", 0), ("host_pin", 0), ("walk_prefetch", 1),
            ("no_such_knob", 1)]
     try:
         for k, v in ok:
@@ -192,12 +190,26 @@ def test_set_tuning_validation():
             assert L.uinet_cksum_set_tuning(k.encode(), v) == u.EINVAL, (k, v)
         assert L.uinet_cksum_set_tuning(None, 1) == u.EINVAL
     finally:  # back to the defaults
-        for k, v in [("blocks_per_cu", 0), ("chains_pass", 2), ("chains_long", 128),
-                     ("chains_tile", 0), ("xcd_remap", 1),
-                     ("host_threads", min(16, os.cpu_count() or 1)), ("walk_prefetch", 1),
-                     ("spans_geo", 0), ("host_pin", 0), ("multi_gather", 0), ("spans_pipe", 1),
-                     ("walk_device", 1)]:
+        for k, v in [("blocks_per_cu", 0), ("chains_long", 128), ("xcd_remap", 1),
+                     ("host_threads", min(16, os.cpu_count() or 1)), ("multi_gather", 0),
+                     ("walk_device", 1), ("chains_wide", 0)]:
             L.uinet_cksum_set_tuning(k.encode(), v)
+
+
+def test_header_lists_at_most_eight_knobs():
+    """The knob list in include/uinet_cksum.h is the set the engine accepts,
+    and it stays short."""
+    import re
+
+    with open(os.path.join(REPO, "include", "uinet_cksum.h")) as f:
+        h = f.read()
+    block = h[h.index("Performance knobs"):h.index("int uinet_cksum_set_tuning")]
+    keys = re.findall(r'^ \*   "(\w+)"', block, re.M)
+    assert 1 <= len(keys) <= 8, keys
+    for k in keys:
+        assert u.lib().uinet_cksum_set_tuning(k.encode(), -12345) == u.EINVAL
+    assert set(keys) == {"blocks_per_cu", "chains_long", "xcd_remap", "host_threads",
+                         "multi_gather", "walk_device", "chains_wide"}
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")

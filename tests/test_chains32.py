@@ -11,7 +11,7 @@ import pytest
 
 import libuinet_amd as u
 
-from test_gpu_parity import HINTS, dev, host16, rand_arena, random_chain_layout
+from test_gpu_parity import HINTS, dev, host16, pad_for_tile, rand_arena, random_chain_layout
 
 
 def packed_dev(torch, seg_off, seg_len):
@@ -83,13 +83,13 @@ def test_chains32_len_skip_seed(torch_dev, ora, hint):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cpass,long_ch,tile", [(2, 128, 0), (2, 16, 8), (2, 0, 32), (4, 128, 0),
-                                                 (4, 16, 8), (4, 0, 32)])
-def test_chains32_long_and_many_segments(torch_dev, ora, cpass, long_ch, tile):
+@pytest.mark.parametrize("long_ch,tile", [(128, 0), (16, 8), (0, 32), (128, 32)])
+def test_chains32_long_and_many_segments(torch_dev, ora, long_ch, tile):
     """Segments up to 65535 B (the u16 limit) mixed with 0..3-B ones, chains of
-    up to 200 segments across descriptor rounds, both batch widths."""
+    up to 200 segments across descriptor rounds, both tile sizes (tile 32: the
+    batch padded with empty chains to 128 K packets)."""
     torch = torch_dev
-    rng = np.random.default_rng(9200 + 7 * cpass + long_ch + tile)
+    rng = np.random.default_rng(9200 + 14 + long_ch + tile)
     arena = rand_arena(1 << 23, 62)
     n = 900
     nseg = rng.integers(0, 200, n)
@@ -106,13 +106,12 @@ def test_chains32_long_and_many_segments(torch_dev, ora, cpass, long_ch, tile):
     skip = np.where(rng.random(n) < 0.5, 20, (rng.random(n) * tot * 0.4).astype(np.int64))
     length = np.where(rng.random(n) < 0.7, tot, skip + (rng.random(n) * (tot - skip + 1)).astype(np.int64))
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    pkt_seg, length, skip, seed = pad_for_tile(tile, pkt_seg, length, skip, seed)
     d_arena, d_ps = dev(torch, arena), dev(torch, pkt_seg.astype(np.int32))
     d_len, d_skip = dev(torch, length.astype(np.int32)), dev(torch, skip.astype(np.int32))
     d_seed = dev(torch, seed.view(np.int32))
     so, sl = packed_dev(torch, seg_off, seg_len)
-    u.set_tuning("chains_pass", cpass)
     u.set_tuning("chains_long", long_ch)
-    u.set_tuning("chains_tile", tile)
     try:
         for flags in (0, u.F_UDP):
             want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip,
@@ -121,9 +120,7 @@ def test_chains32_long_and_many_segments(torch_dev, ora, cpass, long_ch, tile):
                                  flags=flags, len_hint=200)
             np.testing.assert_array_equal(host16(got), want)
     finally:
-        u.set_tuning("chains_pass", 2)
         u.set_tuning("chains_long", 128)
-        u.set_tuning("chains_tile", 0)
 
 
 @pytest.mark.gpu

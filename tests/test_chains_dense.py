@@ -15,7 +15,7 @@ import pytest
 import libuinet_amd as u
 from libuinet_amd.mbuf import aligned_empty
 
-from test_gpu_parity import dev, host16, rand_arena, torch_dev  # noqa: F401
+from test_gpu_parity import dev, host16, pad_for_tile, rand_arena, torch_dev  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 
@@ -78,7 +78,7 @@ def run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip, seed, pack
 
 
 def with_knobs(knobs, fn):
-    dflt = {"chains_tile": 0, "chains_pass": 2, "chains_long": 128}
+    dflt = {"chains_long": 128}
     for k, v in knobs.items():
         u.set_tuning(k, v)
     try:
@@ -101,19 +101,21 @@ def test_dense_layouts(torch_dev, ora, shape):
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("tile,cpass,long_ch", [(8, 2, 128), (32, 4, 128), (32, 2, 16), (8, 4, 0)])
-def test_dense_geometries(torch_dev, ora, tile, cpass, long_ch):
-    """Dense rounds at both tile sizes and batch widths, with long segments
-    (streamed wave-wide) inside the dense run."""
+@pytest.mark.parametrize("tile,long_ch", [(8, 128), (32, 128), (32, 16), (8, 0)])
+def test_dense_geometries(torch_dev, ora, tile, long_ch):
+    """Dense rounds at both tile sizes (tile 32: padded with empty chains to
+    128 K packets), with long segments (streamed wave-wide) inside the dense
+    run."""
     torch = torch_dev
-    rng = np.random.default_rng(13000 + tile + cpass + long_ch)
+    rng = np.random.default_rng(13000 + tile + 2 + long_ch)
     arena = rand_arena(1 << 23, 130)
     seg_off, seg_len, pkt_seg = dense_layout(rng, 3000, arena.size, "in", max_seg=600)
     length, skip, seed = clip_args(rng, seg_len, pkt_seg)
+    pkt_seg, length, skip, seed = pad_for_tile(tile, pkt_seg, length, skip, seed)
     for flags in (0, u.F_UDP):
         want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed,
                           flags=flags)
-        got = with_knobs({"chains_tile": tile, "chains_pass": cpass, "chains_long": long_ch},
+        got = with_knobs({"chains_long": long_ch},
                          lambda: run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip,
                                             seed, False, flags))
         np.testing.assert_array_equal(got, want)
@@ -146,11 +148,11 @@ def test_dense_extremes(torch_dev, ora):
     seg_off[-1] = arena.size - seg_len[-1]  # the last segment ends on the last byte
     seg_off[-2] = seg_off[-1] - seg_len[-2]  # (the last round: scattered, the chunk list)
     length, skip, seed = clip_args(rng, seg_len, pkt_seg)
-    want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
     for tile in (8, 32):
-        got = with_knobs({"chains_tile": tile, "chains_long": 0},
-                         lambda: run_chains(torch, arena, seg_off, seg_len, pkt_seg, length, skip,
-                                            seed, False))
+        ps, ln, sk, sd = pad_for_tile(tile, pkt_seg, length, skip, seed)
+        want = ora.chains(arena, seg_off, seg_len, ps, length=ln, skip=sk, seed=sd)
+        got = with_knobs({"chains_long": 0},
+                         lambda: run_chains(torch, arena, seg_off, seg_len, ps, ln, sk, sd, False))
         np.testing.assert_array_equal(got, want)
 
 

@@ -1,6 +1,6 @@
 """Randomised differential test of the device-resident entry points against the
 oracle: every trial draws an API (spans wide / packed, strided, chains wide /
-packed), a batch shape (counts, length families from empty to 20 KB, head
+packed, HBM mbuf chains), a batch shape (counts, length families from empty to 20 KB, head
 offsets, lengths and skips that cut chains short), a length hint that may not
 match the batch, flags, seeds and parity, and a setting of every performance
 knob (which must never change a result: include/uinet_cksum.h).  Seeded, so a
@@ -18,13 +18,9 @@ from test_gpu_parity import dev, host16, rand_arena
 
 pytestmark = pytest.mark.gpu
 
-DEFAULTS = {"blocks_per_cu": 0, "chains_pass": 2, "chains_long": 128, "chains_tile": 0,
-            "xcd_remap": 1, "spans_geo": 0, "spans_pipe": 1, "chains_wide": 0}
-KNOBS = {"blocks_per_cu": [0, 0, 1, 3, 64], "chains_pass": [2, 2, 4], "chains_long": [128, 0, 16],
-         "chains_tile": [0, 8, 32], "xcd_remap": [1, 0], "spans_pipe": [1, 1, 0],
-         "chains_wide": [0, 0, 1, 2],
-         "spans_geo": [0] * 6 + [4 * 16 + 1, 4 * 16 + 2, 8 * 16 + 1, 8 * 16 + 2, 16 * 16 + 3,
-                                 32 * 16 + 3, 64 * 16 + 2, 64 * 16 + 3, 64 * 16 + 9]}
+DEFAULTS = {"blocks_per_cu": 0, "chains_long": 128, "xcd_remap": 1, "chains_wide": 0}
+KNOBS = {"blocks_per_cu": [0, 0, 1, 3, 64], "chains_long": [128, 0, 16], "xcd_remap": [1, 0],
+         "chains_wide": [0, 0, 1, 2]}
 HINTS = (0, 64, 80, 200, 500, 1500, 4000, 9000)
 ARENA = 8 << 20
 TRIALS = int(os.environ.get("UINET_FUZZ_TRIALS", "300"))  # longer hunts: set it
@@ -45,7 +41,7 @@ def _trial(torch, ora, arena, d_arena, t):
     knobs = {k: int(rng.choice(vals)) for k, vals in KNOBS.items()}
     for k, v in knobs.items():
         u.set_tuning(k, v)
-    api = ("spans", "spans32", "strided", "chains", "chains32")[rng.integers(0, 5)]
+    api = ("spans", "spans32", "strided", "chains", "chains32", "mbufs")[rng.integers(0, 6)]
     n = int(rng.choice([1, 2, 3, 63, 64, 65, int(rng.integers(1, 3000))]))
     hint = int(rng.choice(HINTS)) if rng.random() < 0.8 else int(rng.integers(0, 12000))
     flags = int(rng.choice([0, u.F_UDP, u.F_NO_COMPLEMENT]))
@@ -95,15 +91,23 @@ def _trial(torch, ora, arena, d_arena, t):
         if rng.random() < 0.5:
             skip = np.minimum(rng.integers(0, 61, n), tot if length is None else length)
             skip = skip.astype(np.int64)
-        if api == "chains32":
-            so, sl = u.pack_segments(seg_off, seg_len.astype(np.int32))
-            d_so, d_sl = dev(torch, so), dev(torch, sl)
+        d_len = dev(torch, length.astype(np.int32)) if length is not None else None
+        d_skip = dev(torch, skip.astype(np.int32)) if skip is not None else None
+        if api == "mbufs":  # the same chains as struct mbufs in HBM
+            from libuinet_amd.workloads import device_mbufs
+
+            mb = device_mbufs(d_arena, seg_off, seg_len, pkt_seg,
+                              shuffle=int(rng.integers(0, 99)) if rng.random() < 0.5 else None)
+            got = u.cksum_mbufs(mb["heads"], length=d_len, skip=d_skip, seed=d_seed, flags=flags)
         else:
-            d_so, d_sl = dev(torch, seg_off), dev(torch, seg_len.astype(np.int32))
-        got = u.cksum_chains(d_arena, d_so, d_sl, dev(torch, pkt_seg.astype(np.int32)),
-                             length=dev(torch, length.astype(np.int32)) if length is not None else None,
-                             skip=dev(torch, skip.astype(np.int32)) if skip is not None else None,
-                             seed=d_seed, flags=flags, len_hint=hint)
+            if api == "chains32":
+                so, sl = u.pack_segments(seg_off, seg_len.astype(np.int32))
+                d_so, d_sl = dev(torch, so), dev(torch, sl)
+            else:
+                d_so, d_sl = dev(torch, seg_off), dev(torch, seg_len.astype(np.int32))
+            got = u.cksum_chains(d_arena, d_so, d_sl, dev(torch, pkt_seg.astype(np.int32)),
+                                 length=d_len, skip=d_skip, seed=d_seed, flags=flags,
+                                 len_hint=hint)
         want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed,
                           flags=flags)
     bad = np.flatnonzero(host16(got) != want)
@@ -129,8 +133,7 @@ def test_fuzz_device_entry_points(ora):
             u.set_tuning(k, v)
 
 
-HOST_DEFAULTS = {"host_threads": min(16, os.cpu_count() or 1), "walk_prefetch": 1, "host_pin": 0,
-                 "walk_device": 1}
+HOST_DEFAULTS = {"host_threads": min(16, os.cpu_count() or 1), "walk_device": 1}
 
 
 def _host_trial(ora, arena, t):
@@ -138,9 +141,7 @@ def _host_trial(ora, arena, t):
 
     rng = np.random.default_rng(70000 + BASE + t)
     u.set_tuning("host_threads", int(rng.choice([1, 2, 5, 16])))
-    u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
-    u.set_tuning("host_pin", int(rng.integers(0, 2)))
-    u.set_tuning("walk_device", int(rng.integers(0, 2)))
+    u.set_tuning("walk_device", int(rng.integers(0, 3)))
     n = int(rng.choice([1, 7, 64, int(rng.integers(1, 2500))]))
     nseg = rng.integers(1, int(rng.choice([2, 6, 30])) + 1, n)  # a chain is >= 1 mbuf
     pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
@@ -220,8 +221,7 @@ def test_fuzz_offload_hooks(ora):
         for t in range(max(1, TRIALS // 10)):
             rng = np.random.default_rng(50000 + BASE + t)
             u.set_tuning("host_threads", int(rng.choice([1, 3, 16])))
-            u.set_tuning("walk_prefetch", int(rng.integers(0, 2)))
-            u.set_tuning("walk_device", int(rng.integers(0, 2)))
+            u.set_tuning("walk_device", int(rng.integers(0, 3)))
             # batches of 2,048 frames and more take the device hook when their
             # mbufs are registered (cksum_hookdev.hip); smaller ones the host hook
             n = int(rng.choice([1, 2, int(rng.integers(1, 1500)), int(rng.integers(2048, 3000))]))

@@ -84,10 +84,10 @@ def test_spans_no_seed_no_parity(torch_dev, ora, hint):
     np.testing.assert_array_equal(host16(got), want)
 
 
-@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("pipe", [1])
 @pytest.mark.parametrize("n", [1, 7, 6000, 70001])
 def test_spans_every_kernel(torch_dev, ora, n, pipe):
-    """Every span kernel family (spans_pipe 1 lean / quad, 0 one-shot) at
+    """Every span kernel family (k_spans_lean, k_spans_quad, k_spans) at
     every geometry, and the strided kernel at 64 and 60 B: each
     packet folded exactly once, ragged tails."""
     torch = torch_dev
@@ -96,32 +96,27 @@ def test_spans_every_kernel(torch_dev, ora, n, pipe):
     off, ln = rand_spans(rng, n, arena.size, 1600)
     want = ora.spans(arena, off, ln)
     d_arena = dev(torch, arena)
-    u.set_tuning("spans_pipe", pipe)
-    try:
-        for hint in HINTS:
-            got = u.cksum_spans(d_arena, dev(torch, off), dev(torch, ln.astype(np.int32)),
-                                len_hint=hint)
-            np.testing.assert_array_equal(host16(got), want)
-        m = min(n, (arena.size - 64) // 64)
-        for length in (64, 60):
-            got = u.cksum_strided(d_arena, 64, length, m)
-            want_s = ora.spans(arena, 64 * np.arange(m, dtype=np.int64),
-                               np.full(m, length, np.int64))
-            np.testing.assert_array_equal(host16(got), want_s)
-    finally:
-        u.set_tuning("spans_pipe", 1)
+    for hint in HINTS:
+        got = u.cksum_spans(d_arena, dev(torch, off), dev(torch, ln.astype(np.int32)),
+                            len_hint=hint)
+        np.testing.assert_array_equal(host16(got), want)
+    m = min(n, (arena.size - 64) // 64)
+    for length in (64, 60):
+        got = u.cksum_strided(d_arena, 64, length, m)
+        want_s = ora.spans(arena, 64 * np.arange(m, dtype=np.int64),
+                           np.full(m, length, np.int64))
+        np.testing.assert_array_equal(host16(got), want_s)
 
 
-@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0)])
 def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
-    """The persistent span kernel at 32 and 64 lanes per packet (spans_pipe
-    1 k_spans_lean, the default) and the one-packet-per-group kernel (0), on grids small enough that every wave walks many steps:
+    """The persistent span kernel at 32 and 64 lanes per packet
+    (k_spans_lean), on grids small enough that every wave walks many steps:
     ragged batches, seeds, parity, UDP, spans longer than one round, empty
     spans."""
     torch = torch_dev
     rng = np.random.default_rng(700 + 10 * pipe + bpc)
     arena = rand_arena(1 << 22, 41)
-    u.set_tuning("spans_pipe", pipe)
     u.set_tuning("blocks_per_cu", bpc)
     try:
         for n in (1, 7, 6000, 70001):
@@ -137,14 +132,13 @@ def test_spans_pipe_grids(torch_dev, ora, pipe, bpc):
                 got = u.cksum_spans(d["arena"], d["off"], d["ln"], len_hint=hint)
                 np.testing.assert_array_equal(host16(got), ora.spans(arena, off, ln))
     finally:
-        u.set_tuning("spans_pipe", 1)
         u.set_tuning("blocks_per_cu", 0)
 
 
-@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("pipe,bpc", [(1, 1), (1, 3), (1, 0)])
 def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
-    """The strided API on the persistent kernel (spans_pipe 1 k_spans_lean; 32
-    / 64 lanes per packet) and on the one-shot kernel (0), with grids small
+    """The strided API on the persistent kernel (k_spans_lean; 32 / 64 lanes
+    per packet), with grids small
     enough that every lane group walks many packets: packet lengths of one
     round and of several, aligned and unaligned strides and bases, seeds and
     UDP, ragged counts."""
@@ -152,7 +146,6 @@ def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
     rng = np.random.default_rng(900 + 10 * pipe + bpc)
     arena = rand_arena(24 << 20, 43)
     d_arena = dev(torch, arena)
-    u.set_tuning("spans_pipe", pipe)
     u.set_tuning("blocks_per_cu", bpc)
     try:
         for length, stride, base in ((1500, 1500, 0), (1500, 1514, 14), (1480, 1501, 3),
@@ -166,11 +159,10 @@ def test_strided_pipe_grids(torch_dev, ora, pipe, bpc):
                 want = ora.spans(arena, off, np.full(n, length, np.int64), seed, None, u.F_UDP)
                 np.testing.assert_array_equal(host16(got), want)
     finally:
-        u.set_tuning("spans_pipe", 1)
         u.set_tuning("blocks_per_cu", 0)
 
 
-@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("pipe", [1])
 def test_spans_far_apart(torch_dev, ora, pipe):
     """Neighbouring packets (one wave's pair at 32 lanes per packet, one
     wave's 16 at 4) that lie 4 GiB and more apart in one arena: the lean
@@ -194,7 +186,6 @@ def test_spans_far_apart(torch_dev, ora, pipe):
     off_host = np.where(side == 1, win + o, o).astype(np.int64)
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     par = rng.integers(0, 2, n).astype(np.uint8)
-    u.set_tuning("spans_pipe", pipe)
     try:
         for hint in (64, 1500, 9000):
             got = u.cksum_spans(d, dev(torch, off_dev), dev(torch, ln.astype(np.int32)),
@@ -203,25 +194,22 @@ def test_spans_far_apart(torch_dev, ora, pipe):
             want = ora.spans(host, off_host, ln.astype(np.int64), seed, par, u.F_UDP)
             np.testing.assert_array_equal(host16(got), want)
     finally:
-        u.set_tuning("spans_pipe", 1)
         del d
         torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("pipe,bpc", [(1, 0), (1, 1), (1, 3), (0, 0)])
+@pytest.mark.parametrize("pipe,bpc", [(1, 0), (1, 1), (1, 3)])
 def test_spans_small_packets(torch_dev, ora, pipe, bpc):
     """The small-packet geometries (4, 8 and 16 lanes per packet; the 4-lane
-    shapes run k_spans_quad under spans_pipe=1, k_spans otherwise), also on
+    shapes run k_spans_quad, the 8 and 16 k_spans), also on
     grids small enough that every wave walks many steps: ragged counts, spans
     longer than the geometry's round, empty spans, seeds, parity, UDP; the
     strided API at 64-B packets, 16-B aligned and not."""
     torch = torch_dev
-    u.set_tuning("spans_pipe", pipe)
     u.set_tuning("blocks_per_cu", bpc)
     try:
         _small_packets(torch, ora)
     finally:
-        u.set_tuning("spans_pipe", 1)
         u.set_tuning("blocks_per_cu", 0)
 
 
@@ -337,6 +325,23 @@ def test_strided(torch_dev, ora, stride, length, base):
     d = dev(torch, arena)
     got = u.cksum_strided(d[base:], stride, length, n)
     np.testing.assert_array_equal(host16(got), want)
+
+
+TILE32_MIN = 32 * 4096  # launch_chains_t: 32-packet tiles from this many packets, 8 below
+
+
+def pad_for_tile(tile, pkt_seg, *arrs):
+    """Append empty chains (no segments, zeros in `arrs`) so the chain kernel
+    runs `tile`-packet tiles (the tile follows the batch size, 8 below
+    TILE32_MIN packets); tile 8 / 0 returns the inputs unchanged."""
+    n = pkt_seg.size - 1
+    if tile != 32 or n >= TILE32_MIN:
+        return (pkt_seg, *arrs)
+    pad = TILE32_MIN - n
+    out = [np.concatenate([pkt_seg, np.full(pad, pkt_seg[-1], pkt_seg.dtype)])]
+    for a in arrs:
+        out.append(None if a is None else np.concatenate([a, np.zeros(pad, a.dtype)]))
+    return tuple(out)
 
 
 def random_chain_layout(rng, n, arena_size, max_seg=256, max_segs=8):
@@ -658,12 +663,11 @@ def test_host_batch_chunked(torch_dev, ora, host_threads):
         u.set_tuning("host_threads", 16)
 
 
-@pytest.mark.parametrize("walk_prefetch", [0, 1])
-def test_host_walk_prefetch_variants(torch_dev, ora, walk_prefetch):
-    """Every host-walk prefetch mode gives the oracle's sums: chains longer
+def test_host_walk_prefetch(torch_dev, ora):
+    """The host walk with its header prefetch gives the oracle's sums: chains longer
     than the bytes wanted (the prefetch must stop where the walk stops), short
     chains, len <= skip, and pseudo-header batches, staged and zero-copy."""
-    rng = np.random.default_rng(300 + walk_prefetch)
+    rng = np.random.default_rng(301)
     arena = rand_arena(1 << 22, 300)
     seg_off, seg_len, pkt_seg = random_chain_layout(rng, 20000, arena.size, max_segs=12)
     ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
@@ -678,20 +682,16 @@ def test_host_walk_prefetch_variants(torch_dev, ora, walk_prefetch):
     dst = rng.integers(0, 2**32, ch.n, dtype=np.uint64).astype(np.uint32)
     proto = np.where(rng.random(ch.n) < 0.5, 6, 17).astype(np.uint8)
     want_ph = ora.pseudo_header_batch(ch.heads, plen, off0, src, dst, proto)
-    u.set_tuning("walk_prefetch", walk_prefetch)
-    try:
-        for registered in (False, True):
+    for registered in (False, True):
+        if registered:
+            u.register_host(arena)
+        try:
+            np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, length, skip), want)
+            np.testing.assert_array_equal(
+                u.in_cksum_pseudo_header_batch(ch.heads, plen, off0, src, dst, proto), want_ph)
+        finally:
             if registered:
-                u.register_host(arena)
-            try:
-                np.testing.assert_array_equal(u.in_cksum_skip_batch(ch.heads, length, skip), want)
-                np.testing.assert_array_equal(
-                    u.in_cksum_pseudo_header_batch(ch.heads, plen, off0, src, dst, proto), want_ph)
-            finally:
-                if registered:
-                    u.unregister_host(arena)
-    finally:
-        u.set_tuning("walk_prefetch", 1)
+                u.unregister_host(arena)
 
 
 @pytest.mark.parametrize("host_threads", [2, 16])
@@ -736,16 +736,15 @@ def test_zero_copy_pipeline_ring(torch_dev, ora, host_threads):
         np.testing.assert_array_equal(got[("hdr", k)], want_hdr)
 
 
-@pytest.mark.parametrize("cpass", [2, 4])
-@pytest.mark.parametrize("long_ch,tile", [(0, 32), (16, 8), (16, 32), (64, 0), (200, 8)])
-def test_chains_long_segments(torch_dev, ora, long_ch, tile, cpass):
+@pytest.mark.parametrize("long_ch,n", [(0, 1 << 17), (16, 3000), (16, 1 << 17), (64, 3000),
+                                       (200, 3000)])
+def test_chains_long_segments(torch_dev, ora, long_ch, n):
     """Chains mixing short and long (wave-streamed) segments, with len/skip
-    clipping that cuts into long segments, over both tile sizes and both
-    batch widths (chains_pass) of the chunk-stream kernel."""
+    clipping that cuts into long segments, over both tile sizes of the
+    chunk-stream kernel (8 packets below 128 K packets, 32 from there)."""
     torch = torch_dev
-    rng = np.random.default_rng(5100 + long_ch + tile)
+    rng = np.random.default_rng(5100 + long_ch + n % 97)
     arena = rand_arena(1 << 23, 51)
-    n = 3000
     nseg = rng.integers(1, 7, n)
     pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
     s = int(pkt_seg[-1])
@@ -757,8 +756,6 @@ def test_chains_long_segments(torch_dev, ora, long_ch, tile, cpass):
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed)
     u.set_tuning("chains_long", long_ch)
-    u.set_tuning("chains_tile", tile)
-    u.set_tuning("chains_pass", cpass)
     try:
         for flags in (0, u.F_UDP):
             w = want if flags == 0 else ora.chains(arena, seg_off, seg_len, pkt_seg, length=length,
@@ -772,20 +769,18 @@ def test_chains_long_segments(torch_dev, ora, long_ch, tile, cpass):
             np.testing.assert_array_equal(host16(got), w)
     finally:
         u.set_tuning("chains_long", 128)
-        u.set_tuning("chains_tile", 0)
-        u.set_tuning("chains_pass", 2)
 
 
-@pytest.mark.parametrize("cpass", [2, 4])
 @pytest.mark.parametrize("long_ch", [0, 200])
-def test_chains_full_rounds(torch_dev, ora, long_ch, cpass):
+def test_chains_full_rounds(torch_dev, ora, long_ch):
     """Descriptor rounds whose chunk list is longer than 4096 chunks: 64
     segments of 1900-2031 B each (up to 127 chunks), mixed with rounds of tiny
-    and empty segments."""
+    and empty segments; 128 K packets, so the 32-packet tile (full 64-segment
+    rounds) runs."""
     torch = torch_dev
-    rng = np.random.default_rng(6100 + long_ch + cpass)
+    rng = np.random.default_rng(6100 + long_ch)
     arena = rand_arena(1 << 24, 61)
-    n = 2048
+    n = 1 << 17
     nseg = rng.integers(1, 9, n)
     pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
     s = int(pkt_seg[-1])
@@ -797,8 +792,6 @@ def test_chains_full_rounds(torch_dev, ora, long_ch, cpass):
     length = np.where(rng.random(n) < 0.7, tot, skip + (rng.random(n) * (tot - skip + 1)).astype(np.int64))
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip)
     u.set_tuning("chains_long", long_ch)
-    u.set_tuning("chains_pass", cpass)
-    u.set_tuning("chains_tile", 32)  # 32 packets x ~5 segments: full 64-segment rounds
     try:
         got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off),
                              dev(torch, seg_len.astype(np.int32)),
@@ -808,16 +801,13 @@ def test_chains_full_rounds(torch_dev, ora, long_ch, cpass):
         np.testing.assert_array_equal(host16(got), want)
     finally:
         u.set_tuning("chains_long", 128)
-        u.set_tuning("chains_pass", 2)
-        u.set_tuning("chains_tile", 0)
 
 
-@pytest.mark.parametrize("cpass", [2, 4])
-def test_chains_kernel_variants(torch_dev, ora, cpass):
-    """The chain kernel at both batch widths (chains_pass) on chains of
-    0..150 segments with len/skip/seed and the UDP flag."""
+def test_chains_kernel_variants(torch_dev, ora):
+    """The chain kernel on chains of 0..150 segments with len/skip/seed and
+    the UDP flag."""
     torch = torch_dev
-    rng = np.random.default_rng(8800 + cpass)
+    rng = np.random.default_rng(8802)
     arena = rand_arena(1 << 21, 47)
     n = 1500
     nseg = rng.integers(0, 151, n)
@@ -832,20 +822,16 @@ def test_chains_kernel_variants(torch_dev, ora, cpass):
     skip = (rng.random(n) * (tot + 1) * 0.3).astype(np.int64)
     length = skip + (rng.random(n) * (tot - skip + 10)).astype(np.int64)
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
-    u.set_tuning("chains_pass", cpass)
-    try:
-        for flags in (0, u.F_UDP):
-            want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip,
-                              seed=seed, flags=flags)
-            got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off),
-                                 dev(torch, seg_len.astype(np.int32)),
-                                 dev(torch, pkt_seg.astype(np.int32)),
-                                 length=dev(torch, length.astype(np.int32)),
-                                 skip=dev(torch, skip.astype(np.int32)),
-                                 seed=dev(torch, seed.view(np.int32)), flags=flags, len_hint=120)
-            np.testing.assert_array_equal(host16(got), want)
-    finally:
-        u.set_tuning("chains_pass", 2)
+    for flags in (0, u.F_UDP):
+        want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip,
+                          seed=seed, flags=flags)
+        got = u.cksum_chains(dev(torch, arena), dev(torch, seg_off),
+                             dev(torch, seg_len.astype(np.int32)),
+                             dev(torch, pkt_seg.astype(np.int32)),
+                             length=dev(torch, length.astype(np.int32)),
+                             skip=dev(torch, skip.astype(np.int32)),
+                             seed=dev(torch, seed.view(np.int32)), flags=flags, len_hint=120)
+        np.testing.assert_array_equal(host16(got), want)
 
 
 def test_chains_beyond_4gib_window(torch_dev, ora):
@@ -874,16 +860,11 @@ def test_chains_beyond_4gib_window(torch_dev, ora):
     seed = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     skip = np.full(n, 3, np.int64)
     want = ora.chains(host, seg_off, seg_len, pkt_seg, skip=skip, seed=seed)
-    for cpass in (2, 4):
-        u.set_tuning("chains_pass", cpass)
-        try:
-            got = u.cksum_chains(d, dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
-                                 dev(torch, pkt_seg.astype(np.int32)),
-                                 skip=dev(torch, skip.astype(np.int32)),
-                                 seed=dev(torch, seed.view(np.int32)), len_hint=150)
-        finally:
-            u.set_tuning("chains_pass", 2)
-        np.testing.assert_array_equal(host16(got), want)
+    got = u.cksum_chains(d, dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
+                         dev(torch, pkt_seg.astype(np.int32)),
+                         skip=dev(torch, skip.astype(np.int32)),
+                         seed=dev(torch, seed.view(np.int32)), len_hint=150)
+    np.testing.assert_array_equal(host16(got), want)
     # the wave-per-packet kernel over the same chains (mean segment >= 2 KiB picks it)
     got = u.cksum_chains(d, dev(torch, seg_off), dev(torch, seg_len.astype(np.int32)),
                          dev(torch, pkt_seg.astype(np.int32)), skip=dev(torch, skip.astype(np.int32)),

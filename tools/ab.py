@@ -2,7 +2,7 @@
 """Interleaved A/B of engine tuning variants in ONE process (so DVFS and
 device-to-device spread hit every variant alike).
 
-  python tools/ab.py --config 3 --variants 'chains_pass=2' 'chains_pass=4' 'chains_pass=8'
+  python tools/ab.py --config 3 --variants 'chains_long=128' 'chains_long=0'
 
 Each variant is a comma list of key=value pairs for uinet_cksum_set_tuning;
 the pseudo-key desc=1 launches with packed descriptors (uinet_cksum_spans32 /
@@ -22,9 +22,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 # the engine's knob defaults (include/uinet_cksum.h); host_threads defaults to
 # min(16, hardware threads)
-DEFAULTS = {"blocks_per_cu": 0, "chains_pass": 2, "chains_long": 128, "chains_tile": 0,
-            "xcd_remap": 1, "spans_geo": 0, "spans_pipe": 1,
-            "walk_prefetch": 1, "host_pin": 0, "multi_gather": 0, "chains_wide": 0,
+DEFAULTS = {"blocks_per_cu": 0, "chains_long": 128, "xcd_remap": 1, "multi_gather": 0,
+            "chains_wide": 0, "walk_device": 1,
             "host_threads": min(16, os.cpu_count() or 1)}
 
 
@@ -55,7 +54,7 @@ def main():
                 for v in a.variants]
     # Every key any variant names goes back to its default before each variant
     # is applied.  (Until round 3 a variant inherited the keys the previous one
-    # had set, so e.g. "spans_pipe=1" after "blocks_per_cu=4096" ran at 4096.)
+    # had set, so e.g. "xcd_remap=1" after "blocks_per_cu=4096" ran at 4096.)
     for v in variants:
         for k in v:
             if k == "desc":
