@@ -279,9 +279,12 @@ def layout_floor_line(cfg: str, w, desc: str, kms, form: str = "seglist") -> dic
         # no descriptors: the packet bytes' lines, one 128-B line per mbuf
         # header the walk reads (records 256 B apart: a line each), and the
         # jobs (head u64, len, skip [, seed] per packet)
+        # (a header mbuf that holds its packet's first bytes shares its first
+        # line with them: counted once, with the bytes)
         walked = W.mbufs_walked(lay["seg_len"], lay["pkt_seg"], lay["lens"], skip)
-        floor = fl["arena_bytes"] + 128 * walked + w["n"] * (16 + (4 if seeded else 0))
-        extra = {"mbufs_walked": walked, "header_line_bytes": 128 * walked}
+        own = walked - (w["n"] if w.get("inline_first") is not None else 0)
+        floor = fl["arena_bytes"] + 128 * own + w["n"] * (16 + (4 if seeded else 0))
+        extra = {"mbufs_walked": walked, "header_line_bytes": 128 * own}
     achieved = floor / (float(kms.mean()) * 1e-3) / 1e9
     return {"bytes": floor, "line": 128, **extra,
             "over_algorithmic": round(floor / w["bytes"], 4),
@@ -712,8 +715,14 @@ def run(args, distributed: bool, wd):
     if args.form == "mbufs" and args.config in CHAIN_CONFIGS:
         import libuinet_amd.workloads as W
 
-        # the same chains as struct mbufs in HBM (records in chain order)
-        w.update(W.device_mbufs(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"]))
+        # the same chains as struct mbufs in HBM (records in chain order); 3tx's
+        # 40-B IP + TCP header lives inside its header mbuf (m_pktdat +
+        # max_linkhdr, 104 B into the record, tcp_output.c:844-846), the
+        # payload slices in page clusters
+        inline = W.tx_inline_offset(w["layout"]) if args.config == "3tx" else None
+        w.update(W.device_mbufs(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"],
+                                inline_first=inline))
+        w["inline_first"] = inline
         w["desc"] += "; as struct mbuf chains in HBM, walked on the GPU (m_next / m_data / m_len)"
     launches = [make_launch(args.config, w, args.api, o, args.desc, form=args.form) for o in outs]
     counts = [n] * world

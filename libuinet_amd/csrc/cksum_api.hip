@@ -655,7 +655,6 @@ int zero_copy_batch(Ctx& c, Batch& B, HostPool& pool, int threads, int nch, int 
 // The host thread sleeps in ctx_wait meanwhile.
 
 enum WalkKind { kWalkNone = 0, kWalkSkip = 1, kWalkPseudo = 2 };
-constexpr uint32_t kWalkKMax = 4096;  // longer chains take the host walk
 constexpr int kWalkGroupMin = 16384;  // packets per walk/fold pipeline group, at least
 
 // The HBM work area of a walk + fold of N jobs at K segment slots per job:

@@ -72,7 +72,8 @@ struct DevView {
     R = regs;
     nreg = n;
     if (!m) return;
-    if (!walk_xlate(R, nreg, m, kOffCsumData + 4, &dm)) {
+    // the three 16-B loads below read bytes [0, kOffCsumFlags + 16) of the mbuf
+    if (!walk_xlate(R, nreg, m, kOffCsumFlags + 16, &dm)) {
       bad = kWalkUnmapped;
       m = 0;
       return;

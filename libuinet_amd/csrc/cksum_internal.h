@@ -90,6 +90,7 @@ int launch_chains32(const void* base, const uint32_t* seg_off, const uint16_t* s
 constexpr int kWalkRegionsMax = 256;
 constexpr uint32_t kWalkFallback = 1;  // status[0]: a job the host walk must take
 constexpr uint32_t kWalkUnmapped = 2;  // status[0]: a pointer outside the regions
+constexpr uint32_t kWalkKMax = 4096;   // segment-list rows: longer chains take the host walk
 // Packet i's chain (heads[i], len[i], skip[i], seed[i]; seed may be NULL) into
 // row i of a K-slot segment list in HBM (seg_off relative to lo_dev; pkt_seg
 // [i] = seg_base + i * K, the row's index in a list of which seg_off / seg_len

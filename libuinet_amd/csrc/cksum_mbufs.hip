@@ -31,7 +31,9 @@
 //     the wave's range at once (its job -- head, len, skip, seed -- was
 //     prefetched when it took the previous one), so every lane stays busy
 //     until the range runs dry: the rounds a wave runs are the range's mbufs
-//     / 64, not the longest chain times the packets per lane.
+//     / 64, not the longest chain times the packets per lane.  The range is
+//     handed out longest packet first (per window of 256 packets, by len), so
+//     the last rounds are short chains.
 // Every m_next hop costs one round trip, but 64 chains per wave and every
 // wave of the chip in flight keep ~100 K hops outstanding: the walk runs at
 // the rate HBM delivers the header lines and packet bytes.
@@ -56,9 +58,22 @@ constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr int kPass = 2;                    // 64-chunk passes per pipelined batch
 constexpr int kWin = 64 * kPass;            // chunks per batch
+// Segments of 2 KiB and more are streamed by the whole wave, pipelined across
+// the round's long segments; shorter ones go through the chunk list.  (A first
+// build streamed each long segment on its own, one latency per 4-KiB round:
+// 5tso's mbuf form 0.342 ms; all segments up to 16 KiB through the chunk
+// list, whose per-chunk lookup then runs over 9-KB payloads: 0.388 ms.)
 constexpr uint32_t kLongCh = 128;           // segments of >= 2 KiB stream wave-wide
-constexpr int kLongU = 4;                   // chunks per lane in flight on a long segment
+constexpr int kLongU = 2;                   // chunks per lane per streamed item
 constexpr uint32_t kHopsMax = UINET_CKSUM_MBUF_HOPS_MAX;  // mbufs followed per chain, at most
+constexpr uint32_t kRing = 128;             // jobs a wave holds in LDS
+
+// A wave's queue of jobs (uinet_cksum_mbufs arguments of one packet each).
+struct JobRing {
+  uint64_t head[kRing];
+  int32_t len[kRing], skip[kRing];
+  uint32_t seed[kRing], pkt[kRing];
+};
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short us16x2 __attribute__((ext_vector_type(2)));
 
@@ -70,6 +85,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mb_window_rsrc(uint64_t sbase)
 }
 __device__ __forceinline__ u32x4 mb_load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2);
+}
+
+// Loads from an address held as an integer, in the global address space: a
+// generic pointer made from an integer compiles to a flat load, which counts
+// in lgkmcnt too, so the next LDS wait would also wait for it (the first build
+// exposed every header load's latency at the fold's first LDS read that way).
+typedef __attribute__((address_space(1))) const uint64_t GlobalU64;
+typedef __attribute__((address_space(1))) const int32_t GlobalI32;
+typedef __attribute__((address_space(1))) const u32x4 GlobalChunk;
+__device__ __forceinline__ uint64_t gload_u64(uint64_t a) {
+  return *reinterpret_cast<GlobalU64*>(a);
+}
+__device__ __forceinline__ int32_t gload_i32(uint64_t a) {
+  return *reinterpret_cast<GlobalI32*>(a);
+}
+__device__ __forceinline__ u32x4 gload_chunk(uint64_t a) {
+  return __builtin_nontemporal_load(reinterpret_cast<GlobalChunk*>(a));
 }
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
@@ -101,6 +133,7 @@ __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
   // slot per lane that lanes without a start in the batch write
   __shared__ uint16_t lds_mark[kWaves][kWin + 64];
   __shared__ WalkRegionHost R[kXlate ? kWalkRegionsMax : 1];
+  __shared__ JobRing lds_ring[kWaves];
   if constexpr (kXlate)
     for (int k = (int)threadIdx.x; k < nreg; k += (int)blockDim.x) R[k] = regions[k];
   for (int i = threadIdx.x; i < kWaves * 128; i += blockDim.x) (&lds_acc[0][0])[i] = 0;
@@ -117,22 +150,54 @@ __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
     lane16[q] = s16x2{x, x};
   }
 
-  // the wave's packets [q, qe): q is the next one not yet handed to a lane
+  // The wave's packets [wq, qe) reach the lanes through a ring of jobs in LDS
+  // (head, len, skip, seed, packet index), refilled at the end of a round
+  // with the next 64 packets, longest first (by len[], a counting sort on
+  // eight length classes): a lane whose chain ends takes the ring's next job
+  // at once, so the short packets of a window run while the long ones finish
+  // and the wave's last rounds are short chains, not a 1500-B packet started
+  // late.  The jobs live in LDS, not in registers, so the kernel keeps its
+  // occupancy.
   const uint64_t w0 = (uint64_t)(blockIdx.x * kWaves + wid) * per_wave;
-  uint32_t q = (uint32_t)min(w0, (uint64_t)n);
+  uint32_t wq = (uint32_t)min(w0, (uint64_t)n);
   const uint32_t qe = (uint32_t)min(w0 + per_wave, (uint64_t)n);
   const bool has_len = plen != nullptr;
   uint32_t st = 0;  // this lane's status bits
-
-  // prefetched job (raw values; converted when the lane takes it)
-  uint32_t jp = kNone, jd = 0;
-  uint64_t jh = 0;
-  int32_t jl = 0, js = 0;
-  auto job_load = [&](uint32_t i) {
-    jh = heads[i];
-    jl = has_len ? plen[i] : 0;
-    js = pskip ? pskip[i] : 0;
-    jd = seed ? seed[i] : 0u;
+  JobRing& ring = lds_ring[wid];
+  uint32_t rhd = 0, rtl = 0;  // ring head (next job to take) and tail (wave-uniform)
+  auto fill = [&]() {  // wave-uniform: 64 more jobs when the ring runs below 64
+    if (wq >= qe || rtl - rhd > 64u) return;
+    const uint32_t cnt = min(64u, qe - wq);
+    const uint32_t i = wq + (uint32_t)lane;
+    const bool v = (uint32_t)lane < cnt;
+    uint64_t h = 0;
+    int32_t l = 0, k = 0;
+    uint32_t d = 0;
+    if (v) {
+      h = heads[i];
+      l = has_len ? plen[i] : 0x7fffffff;
+      k = pskip ? pskip[i] : 0;
+      d = seed ? seed[i] : 0u;
+    }
+    const int32_t lc = l < 128 ? 127 : l;
+    const uint32_t b = v ? (uint32_t)min(7, 25 - __builtin_clz((uint32_t)lc)) : 8u;  // 0: < 256 B
+    uint32_t pos = 0, cursor = 0;
+    for (int c = 7; c >= 0; --c) {
+      const uint64_t bm = __ballot(b == (uint32_t)c);
+      if (b == (uint32_t)c) pos = cursor + lane_rank(bm);
+      cursor += (uint32_t)__builtin_popcountll(bm);
+    }
+    if (v) {
+      const uint32_t slot = (rtl + pos) & (kRing - 1);
+      ring.head[slot] = h;
+      ring.len[slot] = l;
+      ring.skip[slot] = k;
+      ring.seed[slot] = d;
+      ring.pkt[slot] = i;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    rtl += cnt;
+    wq += cnt;
   };
   // the current chain
   uint32_t p = kNone, L = 0, S = 0, sd = 0, pos = 0, hops = 0;
@@ -149,45 +214,47 @@ __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
       }
       a = d;
     }
-    hn = *reinterpret_cast<const uint64_t*>(a);        // m_next
-    hd = *reinterpret_cast<const uint64_t*>(a + 16);   // m_data
-    hl = *reinterpret_cast<const int32_t*>(a + 24);    // m_len
+    hn = gload_u64(a);        // m_next
+    hd = gload_u64(a + 16);   // m_data
+    hl = gload_i32(a + 24);   // m_len
   };
-  auto take_job = [&]() {
-    p = jp;
-    m = 0;
-    if (p == kNone) return;
-    int32_t l = has_len ? jl : 0x7fffffff, s = js;
-    L = has_len ? (uint32_t)(l < 0 ? 0 : l) : 0xffffffffu;
-    if (s < 0) {  // outside the contract (the device walk's host mark)
-      st |= kXlate ? kWalkFallback : (uint32_t)UINET_CKSUM_MBUF_BADARG;
-      L = 0;
-      s = 0;
+  // Every lane with `want` takes the ring's next job (wave-uniform call): its
+  // first mbuf's header load goes out at once.
+  auto take_job = [&](bool want) {
+    const uint64_t tm = __ballot(want);
+    if (!tm) return;
+    const uint32_t r = lane_rank(tm), avail = rtl - rhd;
+    if (want) {
+      p = kNone;
+      m = 0;
+      if (r < avail) {
+        const uint32_t slot = (rhd + r) & (kRing - 1);
+        p = ring.pkt[slot];
+        int32_t l = ring.len[slot], k = ring.skip[slot];
+        L = has_len ? (uint32_t)(l < 0 ? 0 : l) : 0xffffffffu;
+        if (k < 0) {  // outside the contract (the device walk's host mark)
+          st |= kXlate ? kWalkFallback : (uint32_t)UINET_CKSUM_MBUF_BADARG;
+          L = 0;
+          k = 0;
+        }
+        S = (uint32_t)k;
+        sd = ring.seed[slot];
+        pos = 0;
+        hops = 0;
+        const uint64_t h = ring.head[slot];
+        if (L > S && h) {  // nothing to read when nothing is summed
+          m = h;
+          hdr_issue(m);
+        }
+      }
     }
-    S = (uint32_t)s;
-    sd = jd;
-    pos = 0;
-    hops = 0;
-    if (L > S && jh) {  // nothing to read when nothing is summed
-      m = jh;
-      hdr_issue(m);
-    }
+    rhd += min((uint32_t)__builtin_popcountll(tm), avail);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   };
-  // start: every lane takes packet q + lane and prefetches q + 64 + lane
-  {
-    const uint32_t i0 = q + (uint32_t)lane, i1 = i0 + 64u;
-    if (i0 < qe) {
-      jp = i0;
-      job_load(i0);
-    }
-    take_job();
-    jp = kNone;
-    if (i1 < qe) {
-      jp = i1;
-      job_load(i1);
-    }
-    q = min(q + 128u, qe);
-  }
+  // start: two windows in the ring, every lane takes its first job
+  fill();
+  fill();
+  take_job(true);
 
   // Chunk-list fold of one round's segments (see cksum_chains.hip,
   // k_chains_pipe, for the addressing and pipelining details).
@@ -262,55 +329,83 @@ __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
       hops++;
       hdr_issue(m);
     }
-    const bool took = fin && jp != kNone;
-    if (fin) take_job();
-    const uint64_t tm = __ballot(took);
-    if (tm) {  // wave-uniform: hand out the next prefetches in lane order
-      const uint32_t idx = q + lane_rank(tm);
-      if (took) {
-        jp = kNone;
-        if (idx < qe) {
-          jp = idx;
-          job_load(idx);
-        }
-      }
-      q = min(q + (uint32_t)__builtin_popcountll(tm), qe);
-    }
+    take_job(fin);
 
-    // --- long segments: one wave-wide stream each ------------------------
+    // --- long segments (>= 2 KiB): one wave-wide stream over all of them -
+    // Items of kLongU chunks per lane, the round's long segments one after
+    // another, item i + 1's loads issued before item i is summed (ping-pong
+    // register sets: a copy of loads in flight would wait for them).
     const bool is_long = nch >= kLongCh;
-    {
+    if (uint64_t lm = __ballot(is_long)) {
       const uint32_t c0_lo = (uint32_t)c0, c0_hi = (uint32_t)(c0 >> 32);
-      for (uint64_t lm = __ballot(is_long); lm; lm &= lm - 1) {
-        const int s = (int)__builtin_ctzll(lm);
-        const uint32_t h = __builtin_amdgcn_readlane(head, s);
-        const uint32_t el = __builtin_amdgcn_readlane(eff, s);
-        const uint32_t mts = __builtin_amdgcn_readlane(meta, s);
-        const uint8_t* cb = reinterpret_cast<const uint8_t*>(readlane_u64(c0_lo, c0_hi, s));
-        const uint32_t nc = __builtin_amdgcn_readlane(nch, s);
-        const uint32_t last_end = ((h + (el & 15u) + 15u) & 15u) + 1u;
-        uint32_t lsum = 0;  // < kLongU * 2^19 per round, folded each round
-        uint64_t tot = 0;
-        for (uint32_t k0 = 0; k0 < nc; k0 += 64 * kLongU) {
-          u32x4 v[kLongU];
+      struct LongSeg {
+        uint64_t cb;
+        uint32_t h, nc, last_end, mts;
+      };
+      auto seg_at = [&](int sl) {
+        LongSeg g;
+        g.h = __builtin_amdgcn_readlane(head, sl);
+        const uint32_t el = __builtin_amdgcn_readlane(eff, sl);
+        g.mts = __builtin_amdgcn_readlane(meta, sl);
+        g.cb = readlane_u64(c0_lo, c0_hi, sl);
+        g.nc = __builtin_amdgcn_readlane(nch, sl);
+        g.last_end = ((g.h + (el & 15u) + 15u) & 15u) + 1u;
+        return g;
+      };
+      auto load = [&](const LongSeg& g, uint32_t k0, u32x4 (&v)[kLongU]) {
 #pragma unroll
-          for (int u = 0; u < kLongU; ++u)
-            if (u == 0 || k0 + 64u * u < nc)
-              v[u] = load_chunk(cb + 16ull * min(k0 + (uint32_t)(u * 64 + lane), nc - 1));
-          lsum = 0;
+        for (int u = 0; u < kLongU; ++u)
+          if (u == 0 || k0 + 64u * u < g.nc)
+            v[u] = gload_chunk(g.cb + 16ull * min(k0 + (uint32_t)(u * 64 + lane), g.nc - 1));
+        asm volatile("" ::: "memory");  // keep the loads here, ahead of the sums
+      };
+      auto sum = [&](const LongSeg& g, uint32_t k0, const u32x4 (&v)[kLongU]) {
+        uint32_t part = 0;  // < kLongU * 2^19
 #pragma unroll
-          for (int u = 0; u < kLongU; ++u) {
-            if (u == 0 || k0 + 64u * u < nc) {
-              const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
-              const int lo_b = k == 0 ? (int)h : (k < nc ? 0 : 16);
-              const int hi_b = k + 1 < nc ? 16 : (k + 1 == nc ? (int)last_end : 0);
-              lsum += lut.sum_oc(v[u], lo_b, hi_b);
-            }
+        for (int u = 0; u < kLongU; ++u) {
+          if (u == 0 || k0 + 64u * u < g.nc) {
+            const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
+            const int lo_b = k == 0 ? (int)g.h : (k < g.nc ? 0 : 16);
+            const int hi_b = k + 1 < g.nc ? 16 : (k + 1 == g.nc ? (int)g.last_end : 0);
+            part += lut.sum_oc(v[u], lo_b, hi_b);
           }
-          tot += lsum;
         }
-        const uint32_t x = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(tot), 0u), 63);
-        if (lane == 0) atomicAdd(&acc[mts], (unsigned long long)x);
+        return part;
+      };
+      int sl = (int)__builtin_ctzll(lm);
+      lm &= lm - 1;
+      LongSeg g = seg_at(sl);
+      uint32_t k0 = 0;
+      uint64_t tot = 0;
+      u32x4 la[kLongU], lb[kLongU];
+      load(g, 0, la);
+      auto step = [&](const u32x4 (&cur)[kLongU], u32x4 (&nxt)[kLongU]) {
+        LongSeg g2 = g;
+        uint32_t k2 = k0 + 64u * kLongU;
+        bool more = true, next_seg = false;
+        if (k2 >= g.nc) {
+          if (lm) {
+            sl = (int)__builtin_ctzll(lm);
+            lm &= lm - 1;
+            g2 = seg_at(sl);
+            k2 = 0;
+            next_seg = true;
+          } else {
+            more = false;
+          }
+        }
+        if (more) load(g2, k2, nxt);
+        tot += sum(g, k0, cur);
+        if (!more || next_seg) {  // the segment's sum into its (lane, parity) bin
+          const uint32_t x = __builtin_amdgcn_readlane(wave_scan<0, false>(fold16(tot), 0u), 63);
+          if (lane == 0) atomicAdd(&acc[g.mts], (unsigned long long)x);
+          tot = 0;
+        }
+        g = g2;
+        k0 = k2;
+        return more;
+      };
+      while (step(la, lb) && step(lb, la)) {
       }
     }
 
@@ -376,8 +471,7 @@ __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
             const uint32_t lo32 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)dk);
             const uint32_t hi32 =
                 (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(dk >> 32));
-            v[k] = load_chunk(reinterpret_cast<const uint8_t*>(
-                (((uint64_t)hi32 << 32) | lo32) + 16ull * cc));
+            v[k] = gload_chunk((((uint64_t)hi32 << 32) | lo32) + 16ull * cc);
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -412,6 +506,9 @@ __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
       acc[2 * lane + 1] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // --- the next 64 jobs into the ring (here, where the round's registers
+    // are dead; the loads wait, once per 64 packets)
+    fill();
   }
   // one atomic per wave, only when something was flagged
   for (int d = 32; d; d >>= 1) st |= (uint32_t)__shfl_xor((int)st, d);

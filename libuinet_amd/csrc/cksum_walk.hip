@@ -72,6 +72,12 @@ __global__ __launch_bounds__(256) void k_walk_mbufs(
     uint64_t cum = 0;
     const size_t row = (size_t)i * K;
     for (uint64_t m = head; !bad && m && cum < lim;) {
+      // a chain no row can hold goes to the host walk: the walk stops here, so
+      // a cyclic or corrupt m_next list cannot keep the kernel running
+      if (cnt >= kWalkKMax) {
+        bad = kWalkFallback;
+        break;
+      }
       uint64_t dm;
       if (!walk_xlate(R, nreg, m, 32, &dm)) {
         bad = kWalkUnmapped;

@@ -305,15 +305,21 @@ def materialize_device(lay, device="cuda"):
 
 # ---- the same chains as struct mbufs in HBM (uinet_cksum_mbufs) ----------------
 
-def device_mbufs(arena, seg_off, seg_len, pkt_seg, shuffle: int | None = None):
+def device_mbufs(arena, seg_off, seg_len, pkt_seg, shuffle: int | None = None,
+                 inline_first: int | None = None):
     """struct mbuf chains in HBM over a device arena, one 256-B record
     (MSIZE, sys/sys/param.h:159) per segment, the way MbufChains lays them out
     on the host: m_next (offset 0) and m_data (16) are DEVICE addresses, m_len
     (24) the segment length, M_PKTHDR in the first mbuf's m_flags (28).
     Records sit in chain order, or -- with ``shuffle`` a seed -- at a random
     permutation of the slots (a UMA zone's free list hands mbufs out in no
-    particular order).  Returns dict(mbufs=int64 tensor (nseg, 32),
-    heads=int64 tensor of the first mbufs' addresses, 0 for an empty chain)."""
+    particular order).  ``inline_first`` = k: every packet's first segment
+    lies INSIDE its own mbuf, k bytes into the record (m_pktdat + max_linkhdr:
+    a header mbuf as tcp_output.c:844-846 builds it, config 3tx's layout puts
+    those records in the arena), so that record is written into the arena at
+    seg_off - k instead of the record array.  Returns dict(mbufs=int64 tensor
+    (nseg, 32), heads=int64 tensor of the first mbufs' addresses, 0 for an
+    empty chain)."""
     import torch
 
     dev = arena.device
@@ -331,19 +337,36 @@ def device_mbufs(arena, seg_off, seg_len, pkt_seg, shuffle: int | None = None):
     nonempty = pkt_seg[1:] > pkt_seg[:-1]
     first = pkt_seg[:-1][nonempty]
     last = pkt_seg[1:][nonempty] - 1
+    if inline_first is not None:
+        rec = seg_off[first] - int(inline_first)
+        if bool((rec < 0).any()) or bool((rec % 8 != 0).any()):
+            raise ValueError("inline_first: records must lie 8-B aligned inside the arena")
+        addr[first] = arena.data_ptr() + rec
     nxt = torch.zeros(nseg, dtype=torch.int64, device=dev)
     if nseg > 1:
         nxt[:-1] = addr[1:]
     nxt[last] = 0
+    flags = torch.zeros(nseg, dtype=torch.int64, device=dev)
+    flags[first] = 0x2  # M_PKTHDR
+    fields = torch.stack([nxt, torch.zeros_like(nxt), arena.data_ptr() + seg_off,
+                          (seg_len & 0xFFFFFFFF) | (flags << 32)], 1)
     if nseg:
-        mb[slot, 0] = nxt
-        mb[slot, 2] = arena.data_ptr() + seg_off
-        flags = torch.zeros(nseg, dtype=torch.int64, device=dev)
-        flags[first] = 0x2  # M_PKTHDR
-        mb[slot, 3] = (seg_len & 0xFFFFFFFF) | (flags << 32)
+        mb[slot, :4] = fields
+    if inline_first is not None and first.numel():
+        # the header mbufs' m_hdr words, written into their records in the arena
+        words = arena.view(-1)[: arena.numel() // 8 * 8].view(torch.int64)
+        w0 = (seg_off[first] - int(inline_first)) // 8
+        for j in range(4):
+            words[w0 + j] = fields[first, j]
     heads = torch.zeros(n, dtype=torch.int64, device=dev)
     heads[nonempty] = addr[first]
     return dict(mbufs=mb, heads=heads)
+
+
+def tx_inline_offset(lay) -> int:
+    """Where config 3tx's header bytes sit in their 256-B header mbuf record
+    (m_pktdat 88 + max_linkhdr 16): device_mbufs(inline_first=...)."""
+    return int(lay["hdr_off"][0] % 256)
 
 
 def mbufs_walked(seg_len, pkt_seg, lens, skip) -> int:

@@ -1,6 +1,9 @@
-"""The device-side chain walk (csrc/cksum_walk.hip): host-mbuf batches whose
-mbufs and packet bytes all lie in registered host memory are walked by the
-GPU (m_next / m_data / m_len read over PCIe) and folded by the chain kernel.
+"""The device-side chain walk: host-mbuf batches whose mbufs and packet bytes
+all lie in registered host memory are walked by the GPU (m_next / m_data /
+m_len read over PCIe) -- in one launch that also folds the bytes
+(csrc/cksum_mbufs.hip, knob walk_device 1, the default) or into a segment
+list that the chain kernel folds (csrc/cksum_walk.hip, walk_device 2); every
+test runs under both.
 Every case is checked bit-exact against the oracle, and
 uinet_cksum_host_cpu().device_walks says whether the GPU walked the batch or
 the host walk took it (a pointer outside the regions, a pseudo-header off0
@@ -53,6 +56,13 @@ def arena(torch_dev):
     return rand_arena(4 << 20, 777)
 
 
+@pytest.fixture(autouse=True, params=[1, 2], ids=["fused", "seglist"])
+def walk_form(request):
+    u.set_tuning("walk_device", request.param)
+    yield request.param
+    u.set_tuning("walk_device", 1)
+
+
 def test_device_walk_skip_batch_edges(ora, arena):
     """Zero-length mbufs, skip exactly on an mbuf boundary, len beyond the
     chain, len < skip, len 0, single-mbuf and long chains."""
@@ -87,10 +97,31 @@ def test_device_walk_long_chains_grow_rows(ora, arena):
     n = 700
     ch, seg_len, pkt_seg = chains(rng, arena, n, max_seg=300, max_len=40)
     with registered(arena, ch.mbufs):
-        u.set_tuning("walk_device", 1)
         got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 30, 3))
     assert nw == 1
     assert np.array_equal(got, ora.skip_batch(ch.heads, 1 << 30, 3))
+
+
+def test_device_walk_chain_past_row_limit(ora, arena, walk_form):
+    """A chain of 5,000 one-byte mbufs among short ones: longer than any
+    segment-list row (4,096), so that walk stops at the limit and hands the
+    batch to the host walk (it never follows a chain without bound); the
+    fused walk takes it on the device.  Same results either way."""
+    rng = np.random.default_rng(12)
+    n = 300
+    nseg = rng.integers(1, 5, n)
+    nseg[137] = 5000
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = rng.integers(1, 100, s)
+    seg_len[pkt_seg[137]:pkt_seg[138]] = 1
+    seg_off = rng.integers(0, arena.size - 101, s).astype(np.int64)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    want = ora.skip_batch(ch.heads, 1 << 30, 2)
+    with registered(arena, ch.mbufs):
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 30, 2))
+    assert nw == (1 if walk_form == 1 else 0)
+    assert np.array_equal(got, want)
 
 
 def test_device_walk_pipelined_groups(ora, arena):
@@ -181,12 +212,9 @@ def test_device_walk_pseudo_header(ora, arena):
 def test_device_walk_knob_off(ora, arena):
     rng = np.random.default_rng(5)
     ch, _, _ = chains(rng, arena, 500)
-    try:
-        u.set_tuning("walk_device", 0)
-        with registered(arena, ch.mbufs):
-            got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 20, 0))
-    finally:
-        u.set_tuning("walk_device", 1)
+    u.set_tuning("walk_device", 0)  # the fixture restores the default
+    with registered(arena, ch.mbufs):
+        got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 20, 0))
     assert nw == 0 and np.array_equal(got, ora.skip_batch(ch.heads, 1 << 20, 0))
 
 

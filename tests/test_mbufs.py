@@ -72,6 +72,28 @@ def test_device_mbufs_records_walk_like_host_chains(ora, shuffle):
     assert slots.size == firsts.size
 
 
+def test_device_mbufs_inline_first_records(ora):
+    """inline_first: each packet's first segment inside its own record (the
+    config-3tx header mbuf); the records written into the arena walk like
+    host chains and leave the summed bytes alone."""
+    lay = W.config3tx_layout(512)
+    arena = W.materialize_host(lay)
+    before = arena.copy()
+    t = torch.from_numpy(arena)
+    d = W.device_mbufs(t, lay["seg_off"], lay["seg_len"], lay["pkt_seg"],
+                       inline_first=W.tx_inline_offset(lay))
+    heads = d["heads"].numpy().view(np.uint64)
+    assert np.array_equal(heads - np.uint64(arena.ctypes.data),
+                          (lay["hdr_off"] - W.tx_inline_offset(lay)).astype(np.uint64))
+    want = ora.chains(before, lay["seg_off"], lay["seg_len"], lay["pkt_seg"], length=lay["lens"],
+                      skip=20)
+    np.testing.assert_array_equal(ora.skip_batch(heads, lay["lens"], 20), want)
+    s, e, _ = W.clipped_segments(lay["seg_off"], lay["seg_len"], lay["pkt_seg"], lay["lens"],
+                                 np.full(512, 20))
+    for a, b in zip(s[:200], e[:200]):
+        assert np.array_equal(arena[a:b], before[a:b])
+
+
 def test_mbufs_walked_counts():
     seg_len = np.array([5, 0, 7, 3, 4, 4], np.int64)
     pkt_seg = np.array([0, 4, 6], np.int64)
@@ -280,7 +302,8 @@ def test_full_chain_variants_mbufs(torch_dev, ora, cfg):
     (TSO segments, pseudo-header seeds) as HBM mbuf chains, full size."""
     w = W.materialize_device(W.chain_layout(cfg))
     lay = w["layout"]
-    d = W.device_mbufs(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"], shuffle=1)
+    d = W.device_mbufs(w["arena"], w["seg_off"], w["seg_len"], w["pkt_seg"], shuffle=1,
+                       inline_first=W.tx_inline_offset(lay) if cfg == "3tx" else None)
     got = host16(u.cksum_mbufs(d["heads"], length=w["len"], skip=w["skip"], seed=w.get("seed")))
     want = ora.chains(w["arena"].cpu().numpy(), lay["seg_off"], lay["seg_len"], lay["pkt_seg"],
                       length=lay["lens"], skip=lay["skip"], seed=lay["seed"])

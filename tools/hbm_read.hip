@@ -304,8 +304,49 @@ static int host(uint64_t bytes) {
   return 0;
 }
 
+// 32-B reads at 256-B slots of an HBM buffer: the mbuf header access of the
+// HBM chain walk (uinet_cksum_mbufs) without its dependency.  Sequential
+// slots (mbufs in chain order, one 32-B header per 256-B record) and random
+// slots; run under rocprofv3 --pmc FETCH_SIZE it calibrates what one such
+// read costs in fetched bytes.
+__global__ __launch_bounds__(256) void k_read_slots_seq(const uint4* __restrict__ p,
+                                                        uint64_t reads,
+                                                        uint32_t* __restrict__ sink) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (uint64_t i = tid; i < 2 * reads; i += nthr) {
+    const uint4 v = p[(i >> 1) * 16 + (i & 1)];
+    acc += v.x + v.y + v.z + v.w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+static int hbm_slots(uint64_t bytes) {
+  uint4* p;
+  uint32_t* sink;
+  CK(hipMalloc(&p, bytes));
+  CK(hipMemset(p, 0x5a, bytes));
+  CK(hipMalloc(&sink, 64));
+  const uint64_t nslot = bytes / 256, reads = nslot;
+  printf("{\"bytes\": %llu, \"memory\": \"HBM\", \"slots\": %llu, \"results\": [\n",
+         (unsigned long long)bytes, (unsigned long long)nslot);
+  bool first = true;
+  for (int g : {4096, 16384, 65536}) {
+    const float ms_seq = time_it([&] { k_read_slots_seq<<<g, 256>>>(p, reads, sink); }, 5);
+    const float ms_rnd = time_it([&] { k_read_slots<<<g, 256>>>(p, nslot, reads, sink); }, 5);
+    printf("%s {\"grid\": %d, \"seq_ms\": %.4f, \"seq_Mreads_per_s\": %.1f, \"rnd_ms\": %.4f, "
+           "\"rnd_Mreads_per_s\": %.1f}\n", first ? "" : ",", g, ms_seq,
+           reads / (ms_seq * 1e-3) / 1e6, ms_rnd, reads / (ms_rnd * 1e-3) / 1e6);
+    first = false;
+  }
+  printf("]}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 2 && !strcmp(argv[1], "host")) return host(strtoull(argv[2], 0, 0));
+  if (argc > 2 && !strcmp(argv[1], "slots")) return hbm_slots(strtoull(argv[2], 0, 0));
   if (argc > 2 && !strcmp(argv[1], "cold")) return cold(atoi(argv[2]));
   if (argc > 3 && !strcmp(argv[1], "cold_valu")) {
     const int k = atoi(argv[3]), n = atoi(argv[2]);

@@ -9,14 +9,19 @@ step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 "$secs" 
   echo "   rc=$rc"; grep -v "^[EW]20" "$OUT/$name.log" | tail -n 2
   case $rc in 0) ;; *) echo FATAL; exit $rc;; esac; }
 for spec in ${CONFIGS:-2 3 3tx 5 5tso}; do
-  # "C" (spans API) or "C@strided"; a "+packed" suffix selects 6-B descriptors
-  desc=wide; case $spec in *+packed) desc=packed; spec=${spec%+packed};; esac
+  # "C" (spans API) or "C@strided"; a "+packed" suffix selects 6-B descriptors,
+  # "+mbufs" the struct mbuf form of a chain config (uinet_cksum_mbufs)
+  desc=wide; form=seglist
+  case $spec in *+packed) desc=packed; spec=${spec%+packed};; esac
+  case $spec in *+mbufs) form=mbufs; spec=${spec%+mbufs};; esac
   c=${spec%@*}; api=spans; [ "$spec" != "$c" ] && api=${spec#*@}
   t=c$c; [ "$api" != spans ] && t=c${c}_$api
   [ "$desc" = packed ] && t=${t}_packed
-  step bench_$t 600 python3 bench.py --config $c --api $api --desc $desc
-  step trace_$t 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$t" -o run --output-format csv -- python3 bench.py --config $c --api $api --desc $desc --cpu-baseline off
-  step pmc_$t 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$t" -o run --output-format csv -- python3 bench.py --config $c --api $api --desc $desc --steps 10 --warmup 2 --cpu-baseline off
+  [ "$form" = mbufs ] && t=${t}_mbufs
+  A="--config $c --api $api --desc $desc --form $form"
+  step bench_$t 600 python3 bench.py $A
+  step trace_$t 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$t" -o run --output-format csv -- python3 bench.py $A --cpu-baseline off
+  step pmc_$t 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$t" -o run --output-format csv -- python3 bench.py $A --steps 10 --warmup 2 --cpu-baseline off
   # the key the bench looks its traffic up by (roofline.traffic_source.key)
   read B KEY <<<"$(python3 -c "import json; d=json.loads([l for l in open('$OUT/bench_$t.log') if l.startswith('{')][-1]); print(d['config']['algorithmic_bytes_per_gpu'], d['roofline']['traffic_source']['key'])")"
   python3 tools/pmc_summary.py "$OUT/pmc_$t" --key "$KEY" --bytes "$B" --out profiles/pmc_traffic.json > "$OUT/pmc_$t.summary.json"
