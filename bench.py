@@ -172,7 +172,8 @@ def make_launch(cfg: str, w, api: str, out, desc: str = "wide", flags: int = 0,
 
     if cfg in CHAIN_CONFIGS and form == "mbufs":
         return lambda s: u.cksum_mbufs(w["heads"], length=w["len"], skip=w["skip"],
-                                       seed=w.get("seed"), out=out, flags=flags, stream=s)
+                                       seed=w.get("seed"), out=out, flags=flags,
+                                       seg_hint=w["hint"], stream=s)
     if cfg in CHAIN_CONFIGS:
         so, sl = (w["seg_off"], w["seg_len"]) if desc == "wide" else w["packed"]
         return lambda s: u.cksum_chains(w["arena"], so, sl, w["pkt_seg"],
@@ -451,11 +452,15 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
         for nt in sorted({1, threads, n_all}):
             for placement in ("pinned", "floating"):
                 pin = (allowed[:nt] if nt > threads else cpus[:nt]) if placement == "pinned" else None
-                rr = [timer(nt, pin, 1) for _ in range(5)]
+                # checksum and read passes alternate (same box conditions for
+                # both), two read passes per checksum pass
+                rr, rd = [], []
+                for _ in range(5):
+                    rr.append(timer(nt, pin, 1))
+                    rd += [R.time_read(host, nthreads=nt, cpus=pin, reps=1) for _ in range(2)]
                 runs[f"{nt}_{placement}"] = float(np.median([r[0] for r in rr]))
                 spread[f"{nt}_{placement}"] = (min(r[0] for r in rr), max(r[0] for r in rr))
                 outs.append(rr[-1][1])
-                rd = [R.time_read(host, nthreads=nt, cpus=pin, reps=1) for _ in range(5)]
                 read[f"{nt}_{placement}"] = (float(np.median(rd)), min(rd))
         best = min((k for k in runs if k.startswith(f"{threads}_")), key=runs.get)
         tn = runs[best]
@@ -505,6 +510,7 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
         # per thread count and placement (median of 5), and its fastest pass:
         # the ceiling every checksum pass above must stay under
         "host_read_gibs": read_gibs or None,
+        "host_read_max_gibs": {k: round(host_gib / b, 3) for k, (_, b) in read.items()} or None,
         "host_read_ceiling_gibs": ceiling or None,
         "fastest_pass_gibs": fastest,
         "within_read_ceiling": (fastest <= ceiling) if ceiling else None,
@@ -520,12 +526,26 @@ def host_offload_line(keep, n: int, nbytes: int, gpu_out, ref_1t_s, reps: int = 
     and the host CPU the call cost (uinet_cksum_host_cpu: calling thread +
     engine pool helpers) per 1,000 packets, beside the reference's 1-thread
     pass over the same mbufs (a scalar loop: its CPU time is its wall time).
+    `bytes_only` repeats it with only the packet bytes registered (the
+    zero-copy netmap setup): the host reads each head mbuf and, one mbuf per
+    packet, hands the GPU spans (uinet_cksum_spans32 descriptors).
     Never `value`; SURVEY.md section 7 step 7 / VERDICT r04 item 1."""
+    ch, args = keep["ch"], keep["args"]
+    link = link_h2d_gbs(keep["host"], [keep["host"], ch.mbufs])
+    row = host_offload_row(keep, [keep["host"], ch.mbufs], n, nbytes, gpu_out, link, reps)
+    row["reference_1thread_ms"] = round(ref_1t_s * 1e3, 3) if ref_1t_s else None
+    row["reference_1thread_cpu_us_per_1k_pkts"] = (round(ref_1t_s * 1e6 / (n / 1000), 3)
+                                                   if ref_1t_s else None)
+    row["bytes_only"] = host_offload_row(keep, [keep["host"]], n, nbytes, gpu_out, link, reps)
+    return row
+
+
+def host_offload_row(keep, bufs, n, nbytes, gpu_out, link, reps):
+    """One host_offload_line measurement with `bufs` registered."""
     import libuinet_amd as u
 
-    ch, args = keep["ch"], keep["args"]
     fn = u.in_cksum_pseudo_header_batch if keep["pseudo"] else u.in_cksum_skip_batch
-    bufs = [keep["host"], ch.mbufs]
+    args = keep["args"]
     for b in bufs:
         u.register_host(b)
     try:
@@ -542,20 +562,24 @@ def host_offload_line(keep, n: int, nbytes: int, gpu_out, ref_1t_s, reps: int = 
     rows.sort(key=lambda r: r[0])
     wall, st, out = rows[len(rows) // 2]
     k = n / 1000
-    link = link_h2d_gbs(keep["host"], bufs)
     return {
-        "what": "the benchmarked batch as host mbufs in registered memory, through the host-mbuf "
-                "batch API (the GPU walks the chains over PCIe); median of %d calls" % reps,
+        "what": "the benchmarked batch as host mbufs (%s registered), through the host-mbuf "
+                "batch API (the GPU reads the bytes in place over PCIe); median of %d calls"
+                % ("packet bytes and mbufs" if len(bufs) > 1 else "packet bytes only", reps),
         "wall_ms": round(wall * 1e3, 3),
         "gibs": round(nbytes / wall / 2**30, 2),
         "host_cpu_us_per_1k_pkts": round(st["cpu_ns"] / 1e3 / k, 3),
+        # which host-resident path the engine took: mbufs registered -> the
+        # GPU walks the chains; bytes only -> one mbuf per packet goes as
+        # spans (the host reads each head mbuf, the link carries the packet
+        # bytes and 6 B per packet), chains to the host walk
+        "path": ("device walk" if st["device_walks"] == st["calls"] else
+                 "single-mbuf spans" if st["span_batches"] == st["calls"] else "host walk"),
         "device_walked": bool(st["device_walks"] == st["calls"]),
-        "reference_1thread_ms": round(ref_1t_s * 1e3, 3) if ref_1t_s else None,
-        "reference_1thread_cpu_us_per_1k_pkts": round(ref_1t_s * 1e6 / k, 3) if ref_1t_s else None,
         "bit_identical": bool(all(np.array_equal(r[2], gpu_out) for r in rows)),
         # the link's own rate, measured here: one DMA copy of the same registered
         # bytes to HBM; the batch's summed bytes over its wall time against it
-        # (the walk's mbuf lines also cross the link and are not counted above)
+        # (mbuf lines the walk reads also cross the link and are not counted)
         "link_h2d_gbs": link,
         "frac_of_link": round(nbytes / wall / 1e9 / link, 4) if link else None,
     }

@@ -156,16 +156,22 @@ int uinet_cksum_device_ok(void);
  *   "host_threads"    host threads that walk/pack a large host-mbuf batch,
  *                     1..64 (default min(16, hardware threads))
  *   "walk_device"     host-mbuf batches (2c, 2d) whose mbufs AND bytes lie in
- *                     registered memory: 1 (default) the GPU walks the chains
- *                     and folds their bytes in one launch, the host only writes
- *                     the jobs; 2 the same as a walk into a segment list, then
- *                     the chain kernel; 0 the host walks them
+ *                     registered memory: the GPU walks the chains, the host
+ *                     only writes the jobs.  3 = walk and fold in one launch;
+ *                     2 = walk into a segment list, then the chain kernel;
+ *                     1 (default) = 2 for chain batches, 3 for the hooks;
+ *                     0 = the host walks them
+ *   "span_fast"       host-mbuf batches (2c, 2d) over registered packet bytes
+ *                     whose every sum lies in the packet's first mbuf (one
+ *                     mbuf per packet, the netmap RX shape): 1 (default) the
+ *                     host reads each head mbuf and the GPU folds the bytes as
+ *                     spans, no mbuf line crosses the link; 0 = the walks below
  *   "multi_gather"    uinet_cksum_spans_multi: 0 = one RCCL gather when it
  *                     applies (default), 1 = always peer copies
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.
  * The environment variables UINET_CKSUM_BLOCKS_PER_CU,
  * UINET_CKSUM_CHAINS_LONG, UINET_CKSUM_CHAINS_WIDE, UINET_CKSUM_XCD_REMAP,
- * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_DEVICE and
+ * UINET_CKSUM_HOST_THREADS, UINET_CKSUM_WALK_DEVICE, UINET_CKSUM_SPAN_FAST and
  * UINET_CKSUM_MULTI_GATHER set the initial values. */
 int uinet_cksum_set_tuning(const char *key, int value);
 
@@ -252,8 +258,10 @@ int uinet_cksum_chains32(const void *base, const uint32_t *seg_off,
  * mbuf, in_cksum.c:254-256).  One launch walks and folds; nothing else is
  * allocated or written.  `status` (a device u32, may be NULL) receives the
  * OR of UINET_CKSUM_MBUF_* bits for inputs outside the reference's contract;
- * it is never cleared here.  The chains are trusted as the reference trusts
- * them: every pointer the walk reaches must be readable device memory. */
+ * it is never cleared here.  `seg_hint` (mean bytes per mbuf, 0 = unknown)
+ * picks the kernel's load policy; it never changes results.  The chains are
+ * trusted as the reference trusts them: every pointer the walk reaches must
+ * be readable device memory. */
 #define UINET_CKSUM_MBUF_TRUNC  0x1u /* a chain of more than UINET_CKSUM_MBUF_HOPS_MAX
                                         mbufs: summed up to there */
 #define UINET_CKSUM_MBUF_BADLEN 0x2u /* a negative m_len: the chain ends there */
@@ -261,7 +269,7 @@ int uinet_cksum_chains32(const void *base, const uint32_t *seg_off,
 #define UINET_CKSUM_MBUF_HOPS_MAX 0x20000u
 int uinet_cksum_mbufs(const struct mbuf *const *heads, const int32_t *len,
     const int32_t *skip, const uint32_t *seed, uint16_t *out, uint32_t n,
-    uint32_t flags, uint32_t *status, void *stream);
+    uint32_t flags, uint32_t seg_hint, uint32_t *status, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* 2c. Host-mbuf batch API (synchronous; for the driver RX/TX batch hooks)   */
@@ -306,8 +314,8 @@ int uinet_cksum_unregister_host(void *base);
 /* tells IPv4 from IPv6 (ip_output's view: 0).  One GPU batch per call;     */
 /* status[i] (may be NULL) receives UINET_RX_* / UINET_TX_* bits.  When the */
 /* mbufs and frames all lie in registered memory (2c) and "walk_device" is  */
-/* 1, the whole hook runs on the GPU -- header parse, walk, fold and the    */
-/* writes into the mbufs -- and the host only copies the mbuf pointers;     */
+/* not 0, the whole hook runs on the GPU -- header parse, walk, fold and    */
+/* the writes into the mbufs -- and the host only copies the mbuf pointers; */
 /* otherwise the host pool parses and walks.  Same results either way.      */
 /* ------------------------------------------------------------------------ */
 
@@ -430,6 +438,8 @@ struct uinet_cksum_host_cpu {
 	uint64_t caller_cpu_ns;  /* the calling thread's CPU time inside them */
 	uint64_t helper_cpu_ns;  /* host-pool helpers' CPU time for them */
 	uint64_t device_walks;   /* calls whose mbuf chains the GPU walked */
+	uint64_t span_batches;   /* calls folded as single-mbuf spans: the host read
+	                            each head mbuf, the GPU the bytes (no walk) */
 };
 
 /* Copies the calling thread's counters to *st (may be NULL) and, when reset

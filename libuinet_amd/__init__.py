@@ -129,7 +129,7 @@ def lib() -> ctypes.CDLL:
         "uinet_cksum_multi_last_gather": (_i32, []),
         "in_cksum_skip_batch_multi": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i32]),
         "uinet_cksum_host_cpu": (_i32, [_vp, _i32]),
-        "uinet_cksum_mbufs": (_i32, [_vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
+        "uinet_cksum_mbufs": (_i32, [_vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -384,7 +384,7 @@ def cksum_chains(base, seg_off, seg_len, pkt_seg, length=None, skip=None, seed=N
 
 
 def cksum_mbufs(heads, length=None, skip=None, seed=None, out=None, flags: int = 0,
-                status=None, stream=None):
+                seg_hint: int = 0, status=None, stream=None):
     """``in_cksum_skip(heads[i], length[i], skip[i])`` (+ ``seed[i]``) over
     struct mbuf chains that live in HBM: ``heads`` is an int64 device tensor
     of first-mbuf device addresses whose m_next / m_data are device addresses
@@ -405,8 +405,8 @@ def cksum_mbufs(heads, length=None, skip=None, seed=None, out=None, flags: int =
         raise ValueError("status needs one element")
     out = _out(n, out, heads)
     _check("uinet_cksum_mbufs", lib().uinet_cksum_mbufs(
-        _dp(heads), _dp(length), _dp(skip), _dp(seed), _dp(out), n, flags, _dp(status),
-        _stream(stream)))
+        _dp(heads), _dp(length), _dp(skip), _dp(seed), _dp(out), n, flags, seg_hint,
+        _dp(status), _stream(stream)))
     return out
 
 
@@ -497,7 +497,7 @@ class HostCpu(ctypes.Structure):
     """struct uinet_cksum_host_cpu (include/uinet_cksum.h section 2f)."""
 
     _fields_ = [("calls", _u64), ("packets", _u64), ("wall_ns", _u64), ("caller_cpu_ns", _u64),
-                ("helper_cpu_ns", _u64), ("device_walks", _u64)]
+                ("helper_cpu_ns", _u64), ("device_walks", _u64), ("span_batches", _u64)]
 
 
 def host_cpu(reset: bool = False) -> dict:

@@ -65,7 +65,7 @@ void note_kernel(const void* host_stub) { t_last_kernel = host_stub; }
 // (tuning()).  The environment seeds them through the same validation.
 struct TuningLive {
   std::atomic<int> blocks_per_cu{0}, host_threads{8}, chains_long{128}, xcd_remap{1},
-      multi_gather{0}, walk_device{1}, chains_wide{0};
+      multi_gather{0}, walk_device{1}, chains_wide{0}, span_fast{1};
 };
 
 static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value) {
@@ -81,8 +81,9 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"xcd_remap", &TuningLive::xcd_remap, [](int v) { return v == 0 || v == 1; }},
       {"host_threads", &TuningLive::host_threads, [](int v) { return v >= 1 && v <= 64; }},
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
-      {"walk_device", &TuningLive::walk_device, [](int v) { return v >= 0 && v <= 2; }},
+      {"walk_device", &TuningLive::walk_device, [](int v) { return v >= 0 && v <= 3; }},
       {"chains_wide", &TuningLive::chains_wide, [](int v) { return v >= 0 && v <= 2; }},
+      {"span_fast", &TuningLive::span_fast, [](int v) { return v == 0 || v == 1; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -98,7 +99,7 @@ static TuningLive& tuning_live() {
         {"UINET_CKSUM_BLOCKS_PER_CU", "blocks_per_cu"}, {"UINET_CKSUM_CHAINS_LONG", "chains_long"},
         {"UINET_CKSUM_XCD_REMAP", "xcd_remap"},         {"UINET_CKSUM_HOST_THREADS", "host_threads"},
         {"UINET_CKSUM_MULTI_GATHER", "multi_gather"},   {"UINET_CKSUM_WALK_DEVICE", "walk_device"},
-        {"UINET_CKSUM_CHAINS_WIDE", "chains_wide"},
+        {"UINET_CKSUM_CHAINS_WIDE", "chains_wide"},     {"UINET_CKSUM_SPAN_FAST", "span_fast"},
     };
     for (const auto& kv : env) {
       const char* e = getenv(kv[0]);
@@ -124,6 +125,7 @@ Tuning tuning() {
   x.multi_gather = ld(t.multi_gather);
   x.walk_device = ld(t.walk_device);
   x.chains_wide = ld(t.chains_wide);
+  x.span_fast = ld(t.span_fast);
   return x;
 }
 
@@ -157,6 +159,7 @@ CpuScope::~CpuScope() {
 }
 
 void note_device_walk() { t_cpu.device_walks++; }
+void note_span_fast() { t_cpu.span_batches++; }
 
 namespace {
 
@@ -300,6 +303,15 @@ int ctx_reserve(Ctx& c, size_t bytes, size_t nout, size_t dbytes = ~size_t(0)) {
     c.out_cap = cap;
   }
   return UINET_CKSUM_OK;
+}
+
+// The batch's results from the mapped result buffer into the caller's array:
+// one bulk copy for u16 results (per-element reads of the pinned buffer cost
+// ~1 ms per million packets).
+void deliver(const Ctx& c, int n, uint16_t* out16, unsigned* out32) {
+  if (out16) memcpy(out16, c.h_out, 2 * (size_t)n);
+  if (out32)
+    for (int i = 0; i < n; i++) out32[i] = c.h_out[i];
 }
 
 // ---- the reference chain walk, emitting the bytes each packet sums --------
@@ -785,7 +797,11 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
   if (nreg_all == 0 || nreg_all > (size_t)kWalkRegionsMax) return kFallback;
   // head(i) is side-effect free (job(i) of a hook parses the frame)
   if (!heads_registered(n, [&](int i) { return head(i).m; })) return kFallback;
-  const bool fused = tuning().walk_device == 1;
+  // the chain batches walk into a segment list by default: over PCIe a
+  // fused wave waits out each hop's round trip between its folds, the walk
+  // kernel keeps a hop per lane in flight (config 3: 9.6 ms against 16.0,
+  // profiles/r06/host_cpu_r06b.md)
+  const bool fused = tuning().walk_device == 3;
   uint32_t K = c.walk_k ? c.walk_k : 4;
   const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const size_t N = (size_t)n;
@@ -846,10 +862,7 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
     if (rc) return rc;
     if (wrc) return wrc;
     if (st[0]) return kFallback;  // a job the host walk must take
-    for (int i = 0; i < n; i++) {
-      if (out16) out16[i] = c.h_out[i];
-      if (out32) out32[i] = c.h_out[i];
-    }
+    deliver(c, n, out16, out32);
     note_device_walk();
     if (trace)
       fprintf(stderr,
@@ -884,10 +897,7 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
     const uint32_t k2 = walk_k_for(longest);
     c.walk_k = k2;
     if (longest <= K) {
-      for (int i = 0; i < n; i++) {
-        if (out16) out16[i] = c.h_out[i];
-        if (out32) out32[i] = c.h_out[i];
-      }
+      deliver(c, n, out16, out32);
       note_device_walk();
       if (trace)
         fprintf(stderr,
@@ -902,6 +912,152 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
     K = k2;  // a chain longer than K: walk again with room for it
   }
   return kFallback;
+}
+
+// ---- single-mbuf spans (host-resident batches whose sums lie in one mbuf) ---
+//
+// The netmap RX shape (uinet_if_netmap.c:1472-1523: one mbuf per received
+// frame) and any batch whose summed bytes all lie in each packet's first
+// mbuf: the host reads each head mbuf's m_next / m_data / m_len (one line it
+// would read to walk anyway), writes a packed span descriptor (u32 offset,
+// u16 length: 6 B) into pinned memory, and the span kernel folds the bytes
+// in place over PCIe.  No mbuf line crosses the link (the device walk moves a
+// 128-B line per mbuf for 32 useful bytes), so the link carries the packet
+// bytes and 6 B per packet.  Pipelined by groups: the host writes group g + 1
+// while the GPU folds group g.  Returns kFallback (stream drained) at
+// the first packet whose sum needs a second mbuf, whose bytes lie outside the
+// registered regions (or, with packed descriptors, in a piece over 65,535 B),
+// or that is outside the
+// reference's contract; the caller then takes the general paths.  Called
+// with g_reg_mu held (shared) and at least one region registered.
+constexpr int kSpanGroup = 1 << 16;  // packets per pipeline group
+template <typename HeadFn, typename JobFn>
+int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, const HeadFn& head,
+                    const JobFn& job, uint16_t* out16, unsigned* out32) {
+  uint64_t lo_addr = ~0ull, hi_addr = 0;
+  for (const Region& r : g_regions) {
+    lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
+    hi_addr = std::max(hi_addr, (uint64_t)(r.end + r.delta));
+  }
+  // packed descriptors (u32 offset, u16 length) when every registered byte
+  // lies within 4 GiB of the lowest, else wide ones (u64, u32: regions far
+  // apart in the address space, e.g. the mbufs registered beside the bytes)
+  const bool packed = hi_addr - lo_addr <= 0x100000000ull;
+  const uint32_t max_span = packed ? 0xffffu : 0x7fffffffu;
+  const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const int G = std::min(n, kSpanGroup);
+  const size_t o_len = a16((packed ? 4 : 8) * (size_t)G);
+  const size_t o_sd = o_len + a16((packed ? 2 : 4) * (size_t)G);
+  const size_t need = o_sd + (seeded ? a16(4 * (size_t)G) : 0);
+  const int groups = (n + G - 1) / G;
+  // every group's descriptors in pinned memory, and their copy in HBM: the
+  // span kernel reads descriptors with scalar loads, each a round trip that
+  // over PCIe its two-step prefetch does not cover (read in place the fold
+  // ran at 47 GB/s); one DMA per group puts them in HBM first
+  int rc = ctx_reserve(c, need * (size_t)groups, (size_t)n, need * (size_t)groups);
+  if (rc) return rc;
+  void* dout = nullptr;
+  rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
+  if (rc) return rc;
+  const std::vector<Region>& regs = g_regions;
+  std::atomic<int> bad{0};
+  for (int g = 0; g < groups; g++) {
+    const int i0 = g * G, ng = std::min(G, n - i0);
+    uint8_t* h = c.h_buf + need * (size_t)g;
+    uint32_t* so = reinterpret_cast<uint32_t*>(h);
+    uint16_t* sl = reinterpret_cast<uint16_t*>(h + o_len);
+    uint64_t* wo = reinterpret_cast<uint64_t*>(h);
+    uint32_t* wl = reinterpret_cast<uint32_t*>(h + o_len);
+    uint32_t* sd = reinterpret_cast<uint32_t*>(h + o_sd);
+    // One thread, the caller: a head mbuf line per packet is all the host
+    // reads, and the GPU's fold of a group takes several times the host's
+    // pass over it, so helpers would only add CPU time (16 threads: 18 us of
+    // CPU per 1,000 packets, one: see DESIGN.md).
+    uint64_t gb = 0;  // the group's summed bytes: its mean span picks the geometry
+    {
+      const Region* last = nullptr;
+      const int a = i0, e = i0 + ng;
+      uint64_t sum = 0;
+      for (int i = a; i < e; i++) {
+        if (i + 8 < e) {
+          const auto r = head(i + 8);
+          if (r.m) __builtin_prefetch(r.m, 0, 3);
+        }
+        const Job J = job(i);
+        const MbufHdr* m = J.m;
+        uint64_t off = 0;
+        uint32_t len = 0;
+        if (J.skip < 0) {
+          bad.store(1, std::memory_order_relaxed);
+          break;
+        }
+        if (m && J.len > J.skip) {
+          // in_cksum.c:203-229 (and :254-272, off0 = skip): the sum stays in
+          // this mbuf when [skip, len) ends in it, or when nothing follows it
+          const long ml = m->m_len, S = J.skip, L = J.len;
+          const bool more = m->m_next != nullptr;
+          const bool second = S < ml ? (L > ml && more)
+                                     : (more || (kind == kWalkPseudo && S > ml));
+          if (ml < 0 || second) {
+            bad.store(1, std::memory_order_relaxed);  // the sum needs a second mbuf
+            break;
+          }
+          if (S < ml) {
+            const long span = std::min(L, ml) - S;
+            uint64_t dev;
+            if (span > (long)max_span ||
+                !device_addr_cached(regs, m->m_data + S, (uint32_t)span, last, &dev)) {
+              bad.store(1, std::memory_order_relaxed);
+              break;
+            }
+            off = dev - lo_addr;
+            len = (uint32_t)span;
+          }
+        }
+        if (packed) {
+          so[i - i0] = (uint32_t)off;
+          sl[i - i0] = (uint16_t)len;
+        } else {
+          wo[i - i0] = off;
+          wl[i - i0] = len;
+        }
+        if (seeded) sd[i - i0] = J.seed;
+        sum += len;
+      }
+      gb = sum;
+    }
+    if (bad.load()) {
+      rc = ctx_wait(c);
+      return rc ? rc : kFallback;
+    }
+    uint8_t* d = c.d_buf + need * (size_t)g;
+    rc = record_hip(hipMemcpyAsync(d, h, need, hipMemcpyHostToDevice, c.stream));
+    if (rc) {
+      (void)ctx_wait(c);
+      return rc;
+    }
+    const uint32_t* dsd = seeded ? reinterpret_cast<const uint32_t*>(d + o_sd) : nullptr;
+    const uint32_t hint = ng ? (uint32_t)(gb / (uint64_t)ng) : 0u;
+    if (packed)
+      rc = launch_spans32(reinterpret_cast<const void*>(lo_addr),
+                          reinterpret_cast<const uint32_t*>(d),
+                          reinterpret_cast<const uint16_t*>(d + o_len), dsd, nullptr,
+                          static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags, hint, c.stream);
+    else
+      rc = launch_spans(reinterpret_cast<const void*>(lo_addr),
+                        reinterpret_cast<const uint64_t*>(d),
+                        reinterpret_cast<const uint32_t*>(d + o_len), dsd, nullptr,
+                        static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags, hint, c.stream);
+    if (rc) {
+      (void)ctx_wait(c);
+      return rc;
+    }
+  }
+  rc = ctx_wait(c);
+  if (rc) return rc;
+  deliver(c, n, out16, out32);
+  note_span_fast();
+  return UINET_CKSUM_OK;
 }
 
 struct ChainRef {
@@ -1011,19 +1167,23 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   // 64 packets 36 / 58 / 42; from 256 packets the device walk leads).
   if (n > stage_below) {
     std::shared_lock<std::shared_mutex> g(g_reg_mu);
+    // mbufs registered: the GPU walks (a few us of host CPU per 1,000
+    // packets); bytes only: single-mbuf sums as spans, then the host walk
+    // (profiles/r06/host_cpu.md)
     if (!g_regions.empty() && kind != kWalkNone && tuning().walk_device) {
       rc = device_walk_batch(c, pool, threads, cs, n, flags, kind, seeded, head, job, out16,
                              out32, trace);
+      if (rc != kFallback) return rc;
+    }
+    if (!g_regions.empty() && kind != kWalkNone && tuning().span_fast) {
+      rc = span_fast_batch(c, n, flags, kind, seeded, head, job, out16, out32);
       if (rc != kFallback) return rc;
     }
     if (!g_regions.empty()) {
       rc = zero_copy_batch(c, B, pool, threads, nch, n, flags, walk_chunk, trace);
       if (rc != kFallback) {
         if (rc) return rc;
-        for (int i = 0; i < n; i++) {
-          if (out16) out16[i] = c.h_out[i];
-          if (out32) out32[i] = c.h_out[i];
-        }
+        deliver(c, n, out16, out32);
         return UINET_CKSUM_OK;
       }
     }
@@ -1141,10 +1301,7 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
             ms(t_start, t_walk), ms(t_walk, t_place), ms(t_place, t_fill), ms(t_fill, t_launch),
             ms(t_launch, t_end));
   }
-  for (int i = 0; i < n; i++) {
-    if (out16) out16[i] = c.h_out[i];
-    if (out32) out32[i] = c.h_out[i];
-  }
+  deliver(c, n, out16, out32);
   return UINET_CKSUM_OK;
 }
 
@@ -1198,7 +1355,9 @@ int run_hook_device(bool rx, struct mbuf* const* mv, int n, int l2len, uint8_t* 
   const size_t d_jd = d_js + a16(4 * J), d_pl = d_jd + a16(4 * J);
   const size_t d_fr = d_pl + a16(hook_plan_bytes(rx) * N), d_res = d_fr + a16(hook_frame_bytes() * N);
   const size_t d_wa = d_res + a16(2 * J);
-  const bool fused = tuning().walk_device == 1;
+  // the hooks fold in the walking launch by default: their chains are one to
+  // three mbufs, and one launch fewer is worth more (profiles/r06/)
+  const bool fused = tuning().walk_device != 2;
   uint32_t K = fused ? 0u : c.walk_k ? c.walk_k : 4;
   if ((uint64_t)J * K > 0xffffffffull) return kFallback;  // rows indexed by u32
   rc = ctx_reserve(c, h_end, N, d_wa + (fused ? 0 : walk_work(J, K).end));
@@ -1442,12 +1601,12 @@ int uinet_cksum_chains32(const void* base, const uint32_t* seg_off, const uint16
 
 int uinet_cksum_mbufs(const struct mbuf* const* heads, const int32_t* len, const int32_t* skip,
                       const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
-                      uint32_t* status, void* stream) {
+                      uint32_t seg_hint, uint32_t* status, void* stream) {
   if (n == 0) return UINET_CKSUM_OK;
   if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
   if (!heads || !out) return UINET_CKSUM_EINVAL;
   return launch_mbufs(reinterpret_cast<const uint64_t*>(heads), len, skip, seed, out, n, flags,
-                      status, static_cast<hipStream_t>(stream));
+                      seg_hint, status, static_cast<hipStream_t>(stream));
 }
 
 // ---- host-mbuf batch API ------------------------------------------------------

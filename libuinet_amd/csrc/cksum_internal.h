@@ -22,9 +22,12 @@ struct Tuning {
                        // segment is 4-9 KiB, 1 = never, 2 = always
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
   int multi_gather;    // uinet_cksum_spans_multi: 0 RCCL gather when it applies, 1 peer copies
-  int walk_device;     // host-mbuf batches in registered memory: 1 the GPU walks and folds
-                       // the chains in one launch (cksum_mbufs.hip), 2 walks them into a
-                       // segment list first (cksum_walk.hip), 0 the host walks them
+  int span_fast;       // host-mbuf batches whose sums lie in the first mbuf: 1 the host
+                       // writes span descriptors (no device walk), 0 off
+  int walk_device;     // host-mbuf batches in registered memory, 0 the host walks them,
+                       // else the GPU: 3 walks and folds in one launch (cksum_mbufs.hip),
+                       // 2 walks into a segment list first (cksum_walk.hip), 1 = 2 for
+                       // the chain batches and 3 for the offload hooks
 };
 Tuning tuning();
 
@@ -111,7 +114,7 @@ int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* 
 // redoes the batch; `pseudo`: the first mbuf must hold skip).
 int launch_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* skip,
                  const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
-                 uint32_t* status, hipStream_t stream);
+                 uint32_t seg_hint, uint32_t* status, hipStream_t stream);
 int launch_mbufs_xlate(const uint64_t* heads, const int32_t* len, const int32_t* skip,
                        const uint32_t* seed, const WalkRegionHost* regions, int nreg, bool pseudo,
                        uint16_t* out, uint32_t n, uint32_t flags, uint32_t* status,

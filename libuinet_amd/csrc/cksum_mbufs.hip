@@ -83,8 +83,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mb_window_rsrc(uint64_t sbase)
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sbase), 0, (int)0xffffffffu,
                                            0x00020000);
 }
+// kTemporal: an ordinary (temporal) load, else non-temporal (aux bit 1).
+template <bool kTemporal>
 __device__ __forceinline__ u32x4 mb_load_chunk_buf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2);
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kTemporal ? 0 : 2);
 }
 
 // Loads from an address held as an integer, in the global address space: a
@@ -100,7 +102,9 @@ __device__ __forceinline__ uint64_t gload_u64(uint64_t a) {
 __device__ __forceinline__ int32_t gload_i32(uint64_t a) {
   return *reinterpret_cast<GlobalI32*>(a);
 }
+template <bool kTemporal = false>
 __device__ __forceinline__ u32x4 gload_chunk(uint64_t a) {
+  if constexpr (kTemporal) return *reinterpret_cast<GlobalChunk*>(a);
   return __builtin_nontemporal_load(reinterpret_cast<GlobalChunk*>(a));
 }
 
@@ -120,7 +124,14 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
 // `pseudo`, the in_cksum_pseudo_header form -- a first mbuf shorter than
 // skip, is reported in status[0] as kWalkUnmapped / kWalkFallback and the
 // host redoes the batch).  Without it they are device addresses used as is.
-template <bool kXlate>
+// kTemporal: the packet-byte loads are ordinary (temporal) loads, else
+// non-temporal.  Short mbufs (config 3's 1-256-B m_fragment pieces) gain from
+// temporal loads -- a chain's next piece, read by the same lane a round later,
+// usually starts in the line this one ends in, still in L2: config 3 0.434 ->
+// 0.375 ms -- and long ones lose (3tx's page slices +8 %, whether chosen per
+// round or per piece inside one kernel; profiles/r06/r06ab_temporal*/).  The
+// caller's seg_hint (mean bytes per mbuf) picks the instantiation.
+template <bool kXlate, bool kTemporal>
 __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
     const uint64_t* __restrict__ heads, const int32_t* __restrict__ plen,
     const int32_t* __restrict__ pskip, const uint32_t* __restrict__ seed,
@@ -466,12 +477,12 @@ __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
                                           __builtin_amdgcn_perm(0u, sc1[k], 0x0c000c0cu), false);
           if constexpr (decltype(kWindow)::value) {
             const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)dkr);
-            v[k] = mb_load_chunk_buf(rsrc, d + 16u * cc);
+            v[k] = mb_load_chunk_buf<kTemporal>(rsrc, d + 16u * cc);
           } else {
             const uint32_t lo32 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)dk);
             const uint32_t hi32 =
                 (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(dk >> 32));
-            v[k] = gload_chunk((((uint64_t)hi32 << 32) | lo32) + 16ull * cc);
+            v[k] = gload_chunk<kTemporal>((((uint64_t)hi32 << 32) | lo32) + 16ull * cc);
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -515,33 +526,43 @@ __global__ __launch_bounds__(kBlock) UINET_MBUFS_OCC void k_mbufs(
   if (status && lane == 0 && st) atomicOr(status, st);
 }
 
-template <bool kXlate>
+template <bool kXlate, bool kTemporal>
 int launch_mbufs_t(const uint64_t* heads, const int32_t* len, const int32_t* skip,
                    const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
                    const WalkRegionHost* regions, int nreg, bool pseudo, uint32_t* status,
                    hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
   // persistent: 5 blocks of 4 waves per CU (the kernel's occupancy), each
-  // wave a contiguous range of packets; small batches get fewer waves, each
-  // with at least 128 packets (two per lane)
+  // wave a contiguous range of packets; batches too small to give every wave
+  // 16 packets get fewer waves.  (At 128 packets per wave, 5tso's 131 K
+  // packets ran on 1,024 waves, one per SIMD: the few lanes of a wave that
+  // hold a packet still stream its long payload wave-wide, so it is the
+  // waves in flight that count.)
   const uint64_t cap = 256ull * (uint64_t)blocks_per_cu(5) * kWaves;
-  uint64_t waves = ((uint64_t)n + 127) / 128;
+  uint64_t waves = ((uint64_t)n + 15) / 16;
   waves = waves < cap ? waves : cap;
   waves = (waves + kWaves - 1) / kWaves * kWaves;
   const uint32_t per_wave = (uint32_t)(((uint64_t)n + waves - 1) / waves);
   const int blocks = (int)(waves / kWaves);
-  UINET_LAUNCH(k_mbufs<kXlate>, dim3(blocks), dim3(kBlock), 0, stream, heads, len, skip, seed,
+  UINET_LAUNCH((k_mbufs<kXlate, kTemporal>), dim3(blocks), dim3(kBlock), 0, stream, heads, len,
+               skip, seed,
                out, n, per_wave, flags, regions, nreg, pseudo ? 1 : 0, status);
   return check_launch();
 }
 
 }  // namespace
 
+// Mean mbuf lengths below this take temporal packet-byte loads (k_mbufs).
+constexpr uint32_t kTemporalSegMax = 256;
+
 int launch_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* skip,
                  const uint32_t* seed, uint16_t* out, uint32_t n, uint32_t flags,
-                 uint32_t* status, hipStream_t stream) {
-  return launch_mbufs_t<false>(heads, len, skip, seed, out, n, flags, nullptr, 0, false, status,
-                               stream);
+                 uint32_t seg_hint, uint32_t* status, hipStream_t stream) {
+  if (seg_hint != 0 && seg_hint < kTemporalSegMax)
+    return launch_mbufs_t<false, true>(heads, len, skip, seed, out, n, flags, nullptr, 0, false,
+                                       status, stream);
+  return launch_mbufs_t<false, false>(heads, len, skip, seed, out, n, flags, nullptr, 0, false,
+                                      status, stream);
 }
 
 int launch_mbufs_xlate(const uint64_t* heads, const int32_t* len, const int32_t* skip,
@@ -549,8 +570,8 @@ int launch_mbufs_xlate(const uint64_t* heads, const int32_t* len, const int32_t*
                        uint16_t* out, uint32_t n, uint32_t flags, uint32_t* status,
                        hipStream_t stream) {
   if (nreg < 1 || nreg > kWalkRegionsMax) return UINET_CKSUM_EINVAL;
-  return launch_mbufs_t<true>(heads, len, skip, seed, out, n, flags, regions, nreg, pseudo,
-                              status, stream);
+  return launch_mbufs_t<true, false>(heads, len, skip, seed, out, n, flags, regions, nreg,
+                                     pseudo, status, stream);
 }
 
 }  // namespace uinet

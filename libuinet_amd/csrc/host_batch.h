@@ -92,6 +92,8 @@ struct CpuScope {
 };
 // The calling thread's batch was walked on the device (counted by the scope).
 void note_device_walk();
+// The calling thread's batch went down the single-mbuf span path.
+void note_span_fast();
 
 // The per-call ABI's host fold (cksum_percall.cpp): one chain on the calling
 // thread, no device involved, no error path (like the reference).

@@ -16,8 +16,8 @@ Engine paths per workload:
   zero_copy   the packet bytes are registered; the host walks the chains and
               writes descriptors, the GPU reads the bytes in place over PCIe
   dev_walk    bytes AND mbufs registered; the GPU walks the chains and folds
-              their bytes in one launch (csrc/cksum_mbufs.hip) -- the host only
-              writes the jobs
+              their bytes in one launch (csrc/cksum_mbufs.hip, knob walk_device
+              3) -- the host only writes the jobs
   dev_walk2   the same, walked into a segment list (csrc/cksum_walk.hip) and
               folded by the chain kernel (knob walk_device 2)
 
@@ -57,6 +57,7 @@ def meter(fn, reps):
     rows.sort(key=lambda r: r[0])
     wall, st = rows[len(rows) // 2]
     return {"wall_ms": round(wall * 1e3, 3), "cpu_ms": round(st["cpu_ns"] / 1e6, 3),
+            "_st": st,
             "caller_cpu_ms": round(st["caller_cpu_ns"] / 1e6, 3),
             "helper_cpu_ms": round(st["helper_cpu_ns"] / 1e6, 3),
             "calls": st["calls"], "device_walks": st["device_walks"],
@@ -102,20 +103,25 @@ PATHS = ("staged", "zero_copy", "dev_walk")
 
 def run_paths(name, n, nbytes, fn, bytes_bufs, mbuf_bufs, threads, reps, check, res):
     """Every engine path x host_threads for one workload; check(out) -> bool."""
-    paths = (("staged", []), ("zero_copy", bytes_bufs), ("dev_walk", bytes_bufs + mbuf_bufs),
-             ("dev_walk2", bytes_bufs + mbuf_bufs))
+    paths = (("staged", []), ("zero_copy", bytes_bufs), ("span", bytes_bufs),
+             ("dev_walk", bytes_bufs + mbuf_bufs), ("dev_walk2", bytes_bufs + mbuf_bufs))
     for path, bufs in paths:
         if path not in PATHS:
             continue
         for t in threads:
             u.set_tuning("host_threads", t)
-            # dev_walk: the fused walk + fold (walk_device 1); dev_walk2: the
+            # dev_walk: the fused walk + fold (walk_device 3); dev_walk2: the
             # walk into a segment list, then the chain kernel (walk_device 2)
-            u.set_tuning("walk_device", 2 if path == "dev_walk2" else 1)
+            u.set_tuning("walk_device", 2 if path == "dev_walk2" else 3)
+            # span: the single-mbuf span path (only one-mbuf sums take it);
+            # the other paths with it off
+            u.set_tuning("span_fast", 1 if path == "span" else 0)
             with Regs(bufs):
                 fn()  # warm: staging buffers, pool threads, walk row size
                 e, out = meter(fn, reps)
             u.set_tuning("walk_device", 1)
+            u.set_tuning("span_fast", 1)
+            e["span_batches"] = e.pop("_st")["span_batches"]
             e = per_k(e, n, nbytes)
             e["bit_identical"] = bool(check(out))
             key = f"{name}/{path}/{t}t"

@@ -172,17 +172,19 @@ def test_set_tuning_validation():
     L = u.lib()
     ok = [("blocks_per_cu", 0), ("blocks_per_cu", 4096), ("chains_long", 0),
           ("chains_long", 16), ("xcd_remap", 0), ("host_threads", 64), ("multi_gather", 1),
-          ("walk_device", 0), ("walk_device", 1), ("walk_device", 2), ("chains_wide", 2)]
+          ("walk_device", 0), ("walk_device", 1), ("walk_device", 2), ("walk_device", 3),
+          ("chains_wide", 2),
+          ("span_fast", 0), ("span_fast", 1)]
     # chains_variant, spans_lut, spans_contig and spans_pipe 2 (k_spans_pp)
     # were removed in round 3; spans_sdesc, host_group and walk_prefetch 2 in
     # round 4; spans_pipe, spans_geo, chains_pass, chains_tile, host_pin and
     # walk_prefetch in round 6 (profiles/r06/pruned/)
     bad = [("blocks_per_cu", -1), ("chains_long", 15), ("xcd_remap", 2), ("host_threads", 0),
            ("spans_sdesc", 0), ("host_group", 1), ("chains_sweep", 2), ("multi_gather", 2),
-           ("chains_variant", 0), ("spans_lut", 1), ("spans_contig", 0), ("walk_device", 3),
+           ("chains_variant", 0), ("spans_lut", 1), ("spans_contig", 0), ("walk_device", 4),
            ("walk_device", -1), ("chains_wide", 3), ("spans_pipe", 1), ("spans_geo", 0),
            ("chains_pass", 2), ("chains_tile", 0), ("host_pin", 0), ("walk_prefetch", 1),
-           ("no_such_knob", 1)]
+           ("span_fast", 2), ("no_such_knob", 1)]
     try:
         for k, v in ok:
             assert L.uinet_cksum_set_tuning(k.encode(), v) == 0, (k, v)
@@ -192,7 +194,7 @@ def test_set_tuning_validation():
     finally:  # back to the defaults
         for k, v in [("blocks_per_cu", 0), ("chains_long", 128), ("xcd_remap", 1),
                      ("host_threads", min(16, os.cpu_count() or 1)), ("multi_gather", 0),
-                     ("walk_device", 1), ("chains_wide", 0)]:
+                     ("walk_device", 1), ("chains_wide", 0), ("span_fast", 1)]:
             L.uinet_cksum_set_tuning(k.encode(), v)
 
 
@@ -209,7 +211,7 @@ def test_header_lists_at_most_eight_knobs():
     for k in keys:
         assert u.lib().uinet_cksum_set_tuning(k.encode(), -12345) == u.EINVAL
     assert set(keys) == {"blocks_per_cu", "chains_long", "xcd_remap", "host_threads",
-                         "multi_gather", "walk_device", "chains_wide"}
+                         "multi_gather", "walk_device", "chains_wide", "span_fast"}
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")

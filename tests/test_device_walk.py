@@ -1,9 +1,9 @@
 """The device-side chain walk: host-mbuf batches whose mbufs and packet bytes
 all lie in registered host memory are walked by the GPU (m_next / m_data /
 m_len read over PCIe) -- in one launch that also folds the bytes
-(csrc/cksum_mbufs.hip, knob walk_device 1, the default) or into a segment
-list that the chain kernel folds (csrc/cksum_walk.hip, walk_device 2); every
-test runs under both.
+(csrc/cksum_mbufs.hip, knob walk_device 3; the hooks' default) or into a
+segment list that the chain kernel folds (csrc/cksum_walk.hip, walk_device 2;
+the chain batches' default); every test runs under both.
 Every case is checked bit-exact against the oracle, and
 uinet_cksum_host_cpu().device_walks says whether the GPU walked the batch or
 the host walk took it (a pointer outside the regions, a pseudo-header off0
@@ -56,11 +56,15 @@ def arena(torch_dev):
     return rand_arena(4 << 20, 777)
 
 
-@pytest.fixture(autouse=True, params=[1, 2], ids=["fused", "seglist"])
+@pytest.fixture(autouse=True, params=[3, 2], ids=["fused", "seglist"])
 def walk_form(request):
+    # the single-mbuf span path (test_span_fast.py) off: every batch here
+    # exercises the device walk, one-mbuf chains included
+    u.set_tuning("span_fast", 0)
     u.set_tuning("walk_device", request.param)
     yield request.param
     u.set_tuning("walk_device", 1)
+    u.set_tuning("span_fast", 1)
 
 
 def test_device_walk_skip_batch_edges(ora, arena):

@@ -98,7 +98,8 @@ def _trial(torch, ora, arena, d_arena, t):
 
             mb = device_mbufs(d_arena, seg_off, seg_len, pkt_seg,
                               shuffle=int(rng.integers(0, 99)) if rng.random() < 0.5 else None)
-            got = u.cksum_mbufs(mb["heads"], length=d_len, skip=d_skip, seed=d_seed, flags=flags)
+            got = u.cksum_mbufs(mb["heads"], length=d_len, skip=d_skip, seed=d_seed, flags=flags,
+                                seg_hint=hint)
         else:
             if api == "chains32":
                 so, sl = u.pack_segments(seg_off, seg_len.astype(np.int32))
@@ -141,7 +142,7 @@ def _host_trial(ora, arena, t):
 
     rng = np.random.default_rng(70000 + BASE + t)
     u.set_tuning("host_threads", int(rng.choice([1, 2, 5, 16])))
-    u.set_tuning("walk_device", int(rng.integers(0, 3)))
+    u.set_tuning("walk_device", int(rng.integers(0, 4)))
     n = int(rng.choice([1, 7, 64, int(rng.integers(1, 2500))]))
     nseg = rng.integers(1, int(rng.choice([2, 6, 30])) + 1, n)  # a chain is >= 1 mbuf
     pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
@@ -221,7 +222,7 @@ def test_fuzz_offload_hooks(ora):
         for t in range(max(1, TRIALS // 10)):
             rng = np.random.default_rng(50000 + BASE + t)
             u.set_tuning("host_threads", int(rng.choice([1, 3, 16])))
-            u.set_tuning("walk_device", int(rng.integers(0, 3)))
+            u.set_tuning("walk_device", int(rng.integers(0, 4)))
             # batches of 2,048 frames and more take the device hook when their
             # mbufs are registered (cksum_hookdev.hip); smaller ones the host hook
             n = int(rng.choice([1, 2, int(rng.integers(1, 1500)), int(rng.integers(2048, 3000))]))

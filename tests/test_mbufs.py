@@ -132,14 +132,14 @@ def host16(t) -> np.ndarray:
 
 
 def run(arena_d, seg_off, seg_len, pkt_seg, length=None, skip=None, seed=None, flags=0,
-        shuffle=None):
+        shuffle=None, seg_hint=0):
     d = W.device_mbufs(arena_d, seg_off, seg_len, pkt_seg, shuffle=shuffle)
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
     got = u.cksum_mbufs(d["heads"],
                         length=None if length is None else dev(np.asarray(length, np.int32)),
                         skip=None if skip is None else dev(np.asarray(skip, np.int32)),
                         seed=None if seed is None else dev(np.asarray(seed, np.uint32).view(np.int32)),
-                        flags=flags, status=st)
+                        flags=flags, seg_hint=seg_hint, status=st)
     torch.cuda.synchronize()
     return host16(got), int(st.item()), d
 
@@ -167,8 +167,9 @@ def test_golden_config3_vectors(torch_dev, arena, golden):
 @pytest.mark.gpu
 @pytest.mark.parametrize("shuffle", [None, 11])
 @pytest.mark.parametrize("flags", [0, u.F_UDP, u.F_NO_COMPLEMENT])
-def test_random_chains(torch_dev, ora, shuffle, flags):
-    rng = np.random.default_rng(70 + flags + (shuffle or 0))
+@pytest.mark.parametrize("seg_hint", [0, 128])  # non-temporal / temporal byte loads
+def test_random_chains(torch_dev, ora, shuffle, flags, seg_hint):
+    rng = np.random.default_rng(70 + flags + (shuffle or 0) + seg_hint)
     arena = rand_arena(1 << 21, 71)
     seg_off, seg_len, pkt_seg = chain_layout(rng, 20000, arena.size)
     length, skip = len_skip(rng, seg_len, pkt_seg)
@@ -177,7 +178,8 @@ def test_random_chains(torch_dev, ora, shuffle, flags):
     seed[rng.random(n) < 0.3] = 0
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=length, skip=skip, seed=seed,
                       flags=flags)
-    got, st, _ = run(dev(arena), seg_off, seg_len, pkt_seg, length, skip, seed, flags, shuffle)
+    got, st, _ = run(dev(arena), seg_off, seg_len, pkt_seg, length, skip, seed, flags, shuffle,
+                     seg_hint)
     np.testing.assert_array_equal(got, want)
     assert st == 0
 
@@ -241,8 +243,9 @@ def test_edge_chains(torch_dev, ora):
     want = ora.chains(arena, seg_off, seg_len, pkt_seg, length=lens, skip=skips)
     ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
     np.testing.assert_array_equal(ora.skip_batch(ch.heads, lens, skips), want)
-    for shuffle in (None, 3):
-        got, st, _ = run(dev(arena), seg_off, seg_len, pkt_seg, lens, skips, shuffle=shuffle)
+    for shuffle, hint in ((None, 0), (3, 100)):
+        got, st, _ = run(dev(arena), seg_off, seg_len, pkt_seg, lens, skips, shuffle=shuffle,
+                         seg_hint=hint)
         np.testing.assert_array_equal(got, want)
         assert st == 0
 
@@ -286,10 +289,11 @@ def test_full_config3_mbufs(torch_dev, ora):
     c = W.config3_device(1 << 20, seed=3)
     lay = c["layout"]
     d = W.device_mbufs(c["arena"], c["seg_off"], c["seg_len"], c["pkt_seg"])
-    got = host16(u.cksum_mbufs(d["heads"], length=c["len"], skip=c["skip"]))
     want = ora.chains(c["arena"].cpu().numpy(), lay["seg_off"], lay["seg_len"], lay["pkt_seg"],
                       length=lay["lens"], skip=20)
-    np.testing.assert_array_equal(got, want)
+    for hint in (0, c["mean_seg"]):
+        got = host16(u.cksum_mbufs(d["heads"], length=c["len"], skip=c["skip"], seg_hint=hint))
+        np.testing.assert_array_equal(got, want)
     seglist = host16(u.cksum_chains(c["arena"], c["seg_off"], c["seg_len"], c["pkt_seg"],
                                     length=c["len"], skip=c["skip"], len_hint=c["mean_seg"]))
     np.testing.assert_array_equal(seglist, want)

@@ -104,12 +104,14 @@ def test_host_batch_multi(torch_dev, ora, devices):
         np.testing.assert_array_equal(got, want)
         # the mbufs registered too: every shard's chains walked by its device
         u.register_host(ch.mbufs)
+        u.set_tuning("span_fast", 0)
         try:
             w0 = u.host_cpu()["device_walks"]
             got = u.in_cksum_skip_batch_multi(devices, ch.heads, lay["lens"], 20)
             if len(devices) == 1:  # one shard: it runs on the calling thread
                 assert u.host_cpu()["device_walks"] == w0 + 1
         finally:
+            u.set_tuning("span_fast", 1)
             u.unregister_host(ch.mbufs)
     finally:
         u.unregister_host(lay["arena"])

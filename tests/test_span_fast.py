@@ -1,0 +1,161 @@
+"""The single-mbuf span path of the host-mbuf batch API (cksum_api.hip,
+span_fast_batch): over registered packet bytes, a batch whose every sum lies
+in its packet's first mbuf is folded as spans -- the host reads each head
+mbuf, the GPU only the bytes.  Bit-exact against the oracle on the edges of
+"lies in the first mbuf" (in_cksum.c:203-229, :254-272), and every batch that
+needs a second mbuf, an unregistered byte or a piece over 65,535 B goes to
+the general paths with the same results."""
+from __future__ import annotations
+
+import contextlib
+
+import numpy as np
+import pytest
+
+import libuinet_amd as u
+from libuinet_amd.mbuf import MbufChains
+
+from test_gpu_parity import rand_arena
+
+pytestmark = pytest.mark.gpu
+
+
+@contextlib.contextmanager
+def registered(*bufs):
+    """`bufs` registered.  With the mbufs registered too the device walk
+    would take the batch first, so it is off inside (the span path then runs
+    with wide descriptors: the regions lie more than 4 GiB apart)."""
+    for b in bufs:
+        u.register_host(b)
+    if len(bufs) > 1:
+        u.set_tuning("walk_device", 0)
+    try:
+        yield
+    finally:
+        u.set_tuning("walk_device", 1)
+        for b in bufs:
+            u.unregister_host(b)
+
+
+def spans(fn):
+    """(result, span batches during fn())."""
+    before = u.host_cpu()["span_batches"]
+    r = fn()
+    return r, u.host_cpu()["span_batches"] - before
+
+
+@pytest.fixture(scope="module")
+def arena(torch_dev):
+    return rand_arena(8 << 20, 991)
+
+
+def _one_mbuf(rng, arena, n, max_len=3000):
+    off = rng.integers(0, arena.size - max_len - 1, n)
+    ln = rng.integers(0, max_len + 1, n)
+    return MbufChains.contiguous(arena, off, ln), ln
+
+
+@pytest.mark.parametrize("mbufs_registered", [False, True])
+def test_span_path_skip_batch(ora, arena, mbufs_registered):
+    """One mbuf per packet at random offsets (odd addresses included), len
+    short of / equal to / beyond the mbuf, skip inside / at / past its end,
+    len <= skip, empty mbufs; with only the bytes or also the mbufs
+    registered (the span path needs only the bytes; the device walk off)."""
+    rng = np.random.default_rng(11)
+    n = 20000
+    ch, ln = _one_mbuf(rng, arena, n)
+    length = np.where(rng.random(n) < 0.2, ln + rng.integers(0, 100, n), ln)
+    length = np.where(rng.random(n) < 0.2, rng.integers(0, ln + 1), length)
+    skip = np.where(rng.random(n) < 0.5, rng.integers(0, 60, n), 0)
+    skip = np.where(rng.random(n) < 0.05, ln, skip)           # skip == m_len
+    skip = np.where(rng.random(n) < 0.05, ln + 7, skip)       # skip past the only mbuf
+    want = ora.skip_batch(ch.heads, length, skip)
+    bufs = (arena, ch.mbufs) if mbufs_registered else (arena,)
+    with registered(*bufs):
+        got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, length, skip))
+    assert ns == 1
+    np.testing.assert_array_equal(got, want)
+
+
+def test_span_path_chained_packets_whose_sum_fits_the_first_mbuf(ora, arena):
+    """Chains of several mbufs whose [skip, len) ends inside the first one
+    (a header-only sum over a TX chain) take the span path; one chain whose
+    sum reaches its second mbuf sends the whole batch to the general path."""
+    rng = np.random.default_rng(12)
+    n = 5000
+    nseg = rng.integers(1, 5, n)
+    pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
+    s = int(pkt_seg[-1])
+    seg_len = rng.integers(40, 400, s)
+    seg_off = rng.integers(0, arena.size - 401, s).astype(np.int64)
+    ch = MbufChains(arena, seg_off, seg_len, pkt_seg)
+    first = seg_len[pkt_seg[:-1]]
+    length = rng.integers(20, first + 1)
+    skip = np.minimum(rng.integers(0, 20, n), length)
+    want = ora.skip_batch(ch.heads, length, skip)
+    with registered(arena):
+        got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, length, skip))
+        assert ns == 1
+        np.testing.assert_array_equal(got, want)
+        length2 = length.copy()
+        length2[n - 3] = first[n - 3] + 5 if nseg[n - 3] > 1 else length2[n - 3]
+        k = int(np.flatnonzero(nseg > 1)[-1])
+        length2[k] = first[k] + 5
+        want2 = ora.skip_batch(ch.heads, length2, skip)
+        got2, ns2 = spans(lambda: u.in_cksum_skip_batch(ch.heads, length2, skip))
+    assert ns2 == 0
+    np.testing.assert_array_equal(got2, want2)
+
+
+def test_span_path_pseudo_header(ora, arena):
+    """in_cksum_pseudo_header_batch over one-mbuf packets (config 5's
+    shape): off0 inside the mbuf and at its end; off0 past it (outside the
+    reference's contract) sends the batch to the general path."""
+    rng = np.random.default_rng(13)
+    n = 6000
+    ch, ln = _one_mbuf(rng, arena, n, max_len=9000)
+    off0 = np.minimum(ln, rng.integers(0, 41, n))
+    plen = np.maximum(0, ln - off0 - rng.integers(0, 30, n))
+    src, dst = (rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) for _ in range(2))
+    proto = rng.choice(np.array([6, 17], np.uint8), n)
+    want = ora.pseudo_header_batch(ch.heads, plen, off0, src, dst, proto)
+    with registered(arena):
+        got, ns = spans(lambda: u.in_cksum_pseudo_header_batch(ch.heads, plen, off0, src, dst,
+                                                                proto))
+        assert ns == 1
+        np.testing.assert_array_equal(got, want)
+
+
+def test_span_path_declines_long_and_unregistered(ora, arena):
+    """A piece over 65,535 B (the packed descriptor's limit) or a byte
+    outside the registered regions: the general path, same results."""
+    rng = np.random.default_rng(14)
+    n = 600
+    big = rand_arena(1 << 20, 15)
+    off = rng.integers(0, arena.size - 70001, n)
+    ln = rng.integers(0, 1500, n)
+    ln[300] = 70000
+    ch = MbufChains.contiguous(arena, off, ln)
+    want = ora.skip_batch(ch.heads, ln, 0)
+    with registered(arena):
+        got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, ln, 0))
+    assert ns == 0
+    np.testing.assert_array_equal(got, want)
+    ch2 = MbufChains.contiguous(big, rng.integers(0, big.size - 1501, n), ln.clip(0, 1500))
+    want2 = ora.skip_batch(ch2.heads, 1500, 0)
+    with registered(arena):  # `big` not registered
+        got2, ns2 = spans(lambda: u.in_cksum_skip_batch(ch2.heads, 1500, 0))
+    assert ns2 == 0
+    np.testing.assert_array_equal(got2, want2)
+
+
+def test_span_path_many_groups(ora, arena):
+    """A batch of several pipeline groups (64 K packets each), ragged tail."""
+    rng = np.random.default_rng(16)
+    n = 3 * 65536 + 777
+    ch, ln = _one_mbuf(rng, arena, n, max_len=1600)
+    want = ora.skip_batch(ch.heads, ln, 0)
+    with registered(arena, ch.mbufs):
+        got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, ln, 0))
+    assert ns == 1
+    np.testing.assert_array_equal(got, want)
