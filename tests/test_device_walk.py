@@ -124,7 +124,7 @@ def test_device_walk_chain_past_row_limit(ora, arena, walk_form):
     want = ora.skip_batch(ch.heads, 1 << 30, 2)
     with registered(arena, ch.mbufs):
         got, nw = walks(lambda: u.in_cksum_skip_batch(ch.heads, 1 << 30, 2))
-    assert nw == (1 if walk_form == 1 else 0)
+    assert nw == (1 if walk_form == 3 else 0)
     assert np.array_equal(got, want)
 
 
