@@ -431,6 +431,8 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
     if keep is not None:
         keep.update(host=host, ch=ch, args=args,
                     pseudo=cfg in ("5", "5tso"))
+        if keep.get("before_passes"):
+            keep["before_passes"]()
     gib = w["bytes"] / 2**30
     runs, spread, read = {}, {}, {}
     if timer is not None:
@@ -518,24 +520,23 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
     }
 
 
-def host_offload_line(keep, n: int, nbytes: int, gpu_out, ref_1t_s, reps: int = 5):
+def host_offload_line(keep, n: int, nbytes: int, gpu_out, reps: int = 5):
     """The benchmarked batch once more as HOST-resident mbufs, the way libuinet
     holds them: packet bytes and mbufs registered with the engine
     (uinet_cksum_register_host), folded through the host-mbuf batch API --
     the GPU walks the chains and reads the bytes over PCIe.  Reports wall time
     and the host CPU the call cost (uinet_cksum_host_cpu: calling thread +
     engine pool helpers) per 1,000 packets, beside the reference's 1-thread
-    pass over the same mbufs (a scalar loop: its CPU time is its wall time).
-    `bytes_only` repeats it with only the packet bytes registered (the
-    zero-copy netmap setup): the host reads each head mbuf and, one mbuf per
-    packet, hands the GPU spans (uinet_cksum_spans32 descriptors).
+    pass over the same mbufs (a scalar loop: its CPU time is its wall time;
+    the caller adds those fields from cpu_baseline's one-thread figure).
+    One mbuf per packet (configs 2, 5) takes the single-mbuf span path: the
+    host reads each head mbuf and hands the GPU spans; chains take the device
+    walk.  `bytes_only` repeats it with only the packet bytes registered (the
+    zero-copy netmap setup: spans, or the host walk for chains).
     Never `value`; SURVEY.md section 7 step 7 / VERDICT r04 item 1."""
     ch, args = keep["ch"], keep["args"]
     link = link_h2d_gbs(keep["host"], [keep["host"], ch.mbufs])
     row = host_offload_row(keep, [keep["host"], ch.mbufs], n, nbytes, gpu_out, link, reps)
-    row["reference_1thread_ms"] = round(ref_1t_s * 1e3, 3) if ref_1t_s else None
-    row["reference_1thread_cpu_us_per_1k_pkts"] = (round(ref_1t_s * 1e6 / (n / 1000), 3)
-                                                   if ref_1t_s else None)
     row["bytes_only"] = host_offload_row(keep, [keep["host"]], n, nbytes, gpu_out, link, reps)
     return row
 
@@ -569,12 +570,12 @@ def host_offload_row(keep, bufs, n, nbytes, gpu_out, link, reps):
         "wall_ms": round(wall * 1e3, 3),
         "gibs": round(nbytes / wall / 2**30, 2),
         "host_cpu_us_per_1k_pkts": round(st["cpu_ns"] / 1e3 / k, 3),
-        # which host-resident path the engine took: mbufs registered -> the
-        # GPU walks the chains; bytes only -> one mbuf per packet goes as
-        # spans (the host reads each head mbuf, the link carries the packet
-        # bytes and 6 B per packet), chains to the host walk
-        "path": ("device walk" if st["device_walks"] == st["calls"] else
-                 "single-mbuf spans" if st["span_batches"] == st["calls"] else "host walk"),
+        # which host-resident path the engine took: one mbuf per packet goes
+        # as spans (the host reads each head mbuf, the link carries the packet
+        # bytes and 6 B per packet); chains to the device walk when the mbufs
+        # are registered, else to the host walk
+        "path": ("single-mbuf spans" if st["span_batches"] == st["calls"] else
+                 "device walk" if st["device_walks"] == st["calls"] else "host walk"),
         "device_walked": bool(st["device_walks"] == st["calls"]),
         "bit_identical": bool(all(np.array_equal(r[2], gpu_out) for r in rows)),
         # the link's own rate, measured here: one DMA copy of the same registered
@@ -884,15 +885,25 @@ def run(args, distributed: bool, wd):
         torch.cuda.synchronize()
         gpu_out = outs[(K - 1) % NBUF].cpu().view(torch.int16).numpy().view(np.uint16)
         keep = {}
+        if args.host_offload == "auto":
+            # the host-resident line runs once the host mbufs exist and before
+            # the reference's passes, whose all-core runs leave the host's
+            # cores clocked down for a while after
+            def before_passes():
+                try:
+                    result["host_resident_cpu"] = host_offload_line(keep, n, w["bytes"], gpu_out)
+                except Exception as e:  # a report, never the measurement: say what failed
+                    result["host_resident_cpu"] = {"error": f"{type(e).__name__}: {e}"}
+            keep["before_passes"] = before_passes
         result["cpu_baseline"] = cpu_baseline(args.config, w, gpu_out, args.cpu_threads, keep)
         result["bit_identical"] = result["cpu_baseline"]["bit_identical_to_gpu"]
-        if args.host_offload == "auto":
-            try:
-                t1 = result["cpu_baseline"].get("one_thread_gibs")
-                ref_1t = w["bytes"] / 2**30 / t1 if t1 else None
-                result["host_resident_cpu"] = host_offload_line(keep, n, w["bytes"], gpu_out, ref_1t)
-            except Exception as e:  # a report, never the measurement: say what failed
-                result["host_resident_cpu"] = {"error": f"{type(e).__name__}: {e}"}
+        h = result.get("host_resident_cpu")
+        if h is not None and "error" not in h:
+            t1 = result["cpu_baseline"].get("one_thread_gibs")
+            ref_1t = w["bytes"] / 2**30 / t1 if t1 else None
+            h["reference_1thread_ms"] = round(ref_1t * 1e3, 3) if ref_1t else None
+            h["reference_1thread_cpu_us_per_1k_pkts"] = (round(ref_1t * 1e6 / (n / 1000), 3)
+                                                         if ref_1t else None)
         result["parity"] = {"packets": n, "against": result["cpu_baseline"]["kind"],
                             "how": "the last timed step's results vs the reference's "
                                    "in_cksum_* over the same bytes as host mbufs"}

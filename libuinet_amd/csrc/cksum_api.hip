@@ -924,63 +924,75 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
 // in place over PCIe.  No mbuf line crosses the link (the device walk moves a
 // 128-B line per mbuf for 32 useful bytes), so the link carries the packet
 // bytes and 6 B per packet.  Pipelined by groups: the host writes group g + 1
-// while the GPU folds group g.  Returns kFallback (stream drained) at
-// the first packet whose sum needs a second mbuf, whose bytes lie outside the
-// registered regions (or, with packed descriptors, in a piece over 65,535 B),
-// or that is outside the
-// reference's contract; the caller then takes the general paths.  Called
-// with g_reg_mu held (shared) and at least one region registered.
+// while the GPU folds group g.  Returns kFallback (stream drained) at the
+// first packet whose sum needs a second mbuf, whose bytes lie outside the
+// registered regions, or that is outside the reference's contract; the
+// caller then takes the general paths.  Called with g_reg_mu held (shared)
+// and at least one region registered.
 constexpr int kSpanGroup = 1 << 16;  // packets per pipeline group
+// Head mbufs are requested this many packets ahead.  One host thread spends
+// ~3 ns per packet and a head mbuf (a DRAM line, often on a page not touched
+// yet) takes ~100-300 ns to arrive, so the distance must cover ~100 packets:
+// config 2, one thread, host CPU per 1,000 packets at distance 8 / 32 / 64 /
+// 128 / 192: 6.3-6.8 / 4.4 / 3.4 / 2.8 / 2.8 us (profiles/r06/r06pf*/).
+constexpr int kSpanPrefetch = 128;
 template <typename HeadFn, typename JobFn>
 int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, const HeadFn& head,
                     const JobFn& job, uint16_t* out16, unsigned* out32) {
-  uint64_t lo_addr = ~0ull, hi_addr = 0;
+  uint64_t lo_addr = ~0ull, hi_addr = 0, big_base = 0, big_len = 0;
   for (const Region& r : g_regions) {
     lo_addr = std::min(lo_addr, (uint64_t)(r.base + r.delta));
     hi_addr = std::max(hi_addr, (uint64_t)(r.end + r.delta));
+    if (r.end - r.base > big_len) {
+      big_len = r.end - r.base;
+      big_base = (uint64_t)(r.base + r.delta);
+    }
   }
-  // packed descriptors (u32 offset, u16 length) when every registered byte
-  // lies within 4 GiB of the lowest, else wide ones (u64, u32: regions far
-  // apart in the address space, e.g. the mbufs registered beside the bytes)
-  const bool packed = hi_addr - lo_addr <= 0x100000000ull;
-  const uint32_t max_span = packed ? 0xffffu : 0x7fffffffu;
-  const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  const int G = std::min(n, kSpanGroup);
-  const size_t o_len = a16((packed ? 4 : 8) * (size_t)G);
-  const size_t o_sd = o_len + a16((packed ? 2 : 4) * (size_t)G);
-  const size_t need = o_sd + (seeded ? a16(4 * (size_t)G) : 0);
-  const int groups = (n + G - 1) / G;
-  // every group's descriptors in pinned memory, and their copy in HBM: the
-  // span kernel reads descriptors with scalar loads, each a round trip that
-  // over PCIe its two-step prefetch does not cover (read in place the fold
-  // ran at 47 GB/s); one DMA per group puts them in HBM first
-  int rc = ctx_reserve(c, need * (size_t)groups, (size_t)n, need * (size_t)groups);
-  if (rc) return rc;
-  void* dout = nullptr;
-  rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
-  if (rc) return rc;
-  const std::vector<Region>& regs = g_regions;
-  std::atomic<int> bad{0};
-  for (int g = 0; g < groups; g++) {
-    const int i0 = g * G, ng = std::min(G, n - i0);
-    uint8_t* h = c.h_buf + need * (size_t)g;
-    uint32_t* so = reinterpret_cast<uint32_t*>(h);
-    uint16_t* sl = reinterpret_cast<uint16_t*>(h + o_len);
-    uint64_t* wo = reinterpret_cast<uint64_t*>(h);
-    uint32_t* wl = reinterpret_cast<uint32_t*>(h + o_len);
-    uint32_t* sd = reinterpret_cast<uint32_t*>(h + o_sd);
-    // One thread, the caller: a head mbuf line per packet is all the host
-    // reads, and the GPU's fold of a group takes several times the host's
-    // pass over it, so helpers would only add CPU time (16 threads: 18 us of
-    // CPU per 1,000 packets, one: see DESIGN.md).
-    uint64_t gb = 0;  // the group's summed bytes: its mean span picks the geometry
-    {
+  // Packed descriptors (u32 offset, u16 length) from a base every summed
+  // byte lies within 4 GiB of: the lowest registered byte when all regions
+  // fit that window, else the largest region's start (the packet arena, with
+  // the mbufs registered elsewhere); a span outside it sends the batch round
+  // once more with wide descriptors (u64, u32).
+  const bool all_packed = hi_addr - lo_addr <= 0x100000000ull;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const bool packed = attempt == 0;
+    const uint64_t base = packed && !all_packed ? big_base : lo_addr;
+    bool outside = false;  // packed: a span outside [base, base + 4 GiB)
+    const uint32_t max_span = packed ? 0xffffu : 0x7fffffffu;
+    const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+    const int G = std::min(n, kSpanGroup);
+    const size_t o_len = a16((packed ? 4 : 8) * (size_t)G);
+    const size_t o_sd = o_len + a16((packed ? 2 : 4) * (size_t)G);
+    const size_t need = o_sd + (seeded ? a16(4 * (size_t)G) : 0);
+    const int groups = (n + G - 1) / G;
+    // every group's descriptors in pinned memory, and their copy in HBM: the
+    // span kernel reads descriptors with scalar loads, each a round trip that
+    // over PCIe its two-step prefetch does not cover (read in place the fold
+    // ran at 47 GB/s); one DMA per group puts them in HBM first
+    int rc = ctx_reserve(c, need * (size_t)groups, (size_t)n, need * (size_t)groups);
+    if (rc) return rc;
+    void* dout = nullptr;
+    rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
+    if (rc) return rc;
+    const std::vector<Region>& regs = g_regions;
+    bool bad = false;
+    for (int g = 0; g < groups && !bad && !outside; g++) {
+      const int i0 = g * G, ng = std::min(G, n - i0);
+      uint8_t* h = c.h_buf + need * (size_t)g;
+      uint32_t* so = reinterpret_cast<uint32_t*>(h);
+      uint16_t* sl = reinterpret_cast<uint16_t*>(h + o_len);
+      uint64_t* wo = reinterpret_cast<uint64_t*>(h);
+      uint32_t* wl = reinterpret_cast<uint32_t*>(h + o_len);
+      uint32_t* sd = reinterpret_cast<uint32_t*>(h + o_sd);
+      // One thread, the caller: a head mbuf line per packet is all the host
+      // reads, and the GPU's fold of a group takes longer than the host's
+      // pass over it, so helpers would only add CPU time.
+      uint64_t gb = 0;  // the group's summed bytes: its mean span picks the geometry
       const Region* last = nullptr;
-      const int a = i0, e = i0 + ng;
-      uint64_t sum = 0;
-      for (int i = a; i < e; i++) {
-        if (i + 8 < e) {
-          const auto r = head(i + 8);
+      const int e = i0 + ng;
+      for (int i = i0; i < e; i++) {
+        if (i + kSpanPrefetch < e) {
+          const auto r = head(i + kSpanPrefetch);
           if (r.m) __builtin_prefetch(r.m, 0, 3);
         }
         const Job J = job(i);
@@ -988,7 +1000,7 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
         uint64_t off = 0;
         uint32_t len = 0;
         if (J.skip < 0) {
-          bad.store(1, std::memory_order_relaxed);
+          bad = true;
           break;
         }
         if (m && J.len > J.skip) {
@@ -999,18 +1011,23 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
           const bool second = S < ml ? (L > ml && more)
                                      : (more || (kind == kWalkPseudo && S > ml));
           if (ml < 0 || second) {
-            bad.store(1, std::memory_order_relaxed);  // the sum needs a second mbuf
+            bad = true;  // the sum needs a second mbuf
             break;
           }
           if (S < ml) {
             const long span = std::min(L, ml) - S;
             uint64_t dev;
-            if (span > (long)max_span ||
+            if (span > 0x7fffffffL ||
                 !device_addr_cached(regs, m->m_data + S, (uint32_t)span, last, &dev)) {
-              bad.store(1, std::memory_order_relaxed);
+              bad = true;
               break;
             }
-            off = dev - lo_addr;
+            if (span > (long)max_span || dev < base ||
+                dev - base + (uint64_t)span > 0x100000000ull) {
+              outside = true;  // packed only: wide descriptors take any of these
+              break;
+            }
+            off = dev - base;
             len = (uint32_t)span;
           }
         }
@@ -1022,42 +1039,41 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
           wl[i - i0] = len;
         }
         if (seeded) sd[i - i0] = J.seed;
-        sum += len;
+        gb += len;
       }
-      gb = sum;
-    }
-    if (bad.load()) {
-      rc = ctx_wait(c);
-      return rc ? rc : kFallback;
-    }
-    uint8_t* d = c.d_buf + need * (size_t)g;
-    rc = record_hip(hipMemcpyAsync(d, h, need, hipMemcpyHostToDevice, c.stream));
-    if (rc) {
-      (void)ctx_wait(c);
-      return rc;
-    }
-    const uint32_t* dsd = seeded ? reinterpret_cast<const uint32_t*>(d + o_sd) : nullptr;
-    const uint32_t hint = ng ? (uint32_t)(gb / (uint64_t)ng) : 0u;
-    if (packed)
-      rc = launch_spans32(reinterpret_cast<const void*>(lo_addr),
-                          reinterpret_cast<const uint32_t*>(d),
-                          reinterpret_cast<const uint16_t*>(d + o_len), dsd, nullptr,
+      if (bad || outside) break;
+      uint8_t* d = c.d_buf + need * (size_t)g;
+      rc = record_hip(hipMemcpyAsync(d, h, need, hipMemcpyHostToDevice, c.stream));
+      if (rc) {
+        (void)ctx_wait(c);
+        return rc;
+      }
+      const uint32_t* dsd = seeded ? reinterpret_cast<const uint32_t*>(d + o_sd) : nullptr;
+      const uint32_t hint = ng ? (uint32_t)(gb / (uint64_t)ng) : 0u;
+      if (packed)
+        rc = launch_spans32(reinterpret_cast<const void*>(base),
+                            reinterpret_cast<const uint32_t*>(d),
+                            reinterpret_cast<const uint16_t*>(d + o_len), dsd, nullptr,
+                            static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags, hint, c.stream);
+      else
+        rc = launch_spans(reinterpret_cast<const void*>(base),
+                          reinterpret_cast<const uint64_t*>(d),
+                          reinterpret_cast<const uint32_t*>(d + o_len), dsd, nullptr,
                           static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags, hint, c.stream);
-    else
-      rc = launch_spans(reinterpret_cast<const void*>(lo_addr),
-                        reinterpret_cast<const uint64_t*>(d),
-                        reinterpret_cast<const uint32_t*>(d + o_len), dsd, nullptr,
-                        static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags, hint, c.stream);
-    if (rc) {
-      (void)ctx_wait(c);
-      return rc;
+      if (rc) {
+        (void)ctx_wait(c);
+        return rc;
+      }
     }
+    rc = ctx_wait(c);  // the groups launched so far (their buffers are reused)
+    if (rc) return rc;
+    if (bad) return kFallback;
+    if (outside) continue;
+    deliver(c, n, out16, out32);
+    note_span_fast();
+    return UINET_CKSUM_OK;
   }
-  rc = ctx_wait(c);
-  if (rc) return rc;
-  deliver(c, n, out16, out32);
-  note_span_fast();
-  return UINET_CKSUM_OK;
+  return kFallback;
 }
 
 struct ChainRef {
@@ -1167,16 +1183,17 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
   // 64 packets 36 / 58 / 42; from 256 packets the device walk leads).
   if (n > stage_below) {
     std::shared_lock<std::shared_mutex> g(g_reg_mu);
-    // mbufs registered: the GPU walks (a few us of host CPU per 1,000
-    // packets); bytes only: single-mbuf sums as spans, then the host walk
-    // (profiles/r06/host_cpu.md)
+    // Single-mbuf sums as spans first (no mbuf line crosses the link: config
+    // 2 at 0.87 of it for ~3 us of host CPU per 1,000 packets), then the
+    // device walk when the mbufs are registered too, then the host walk
+    // (profiles/r06/NOTES.md)
+    if (!g_regions.empty() && kind != kWalkNone && tuning().span_fast) {
+      rc = span_fast_batch(c, n, flags, kind, seeded, head, job, out16, out32);
+      if (rc != kFallback) return rc;
+    }
     if (!g_regions.empty() && kind != kWalkNone && tuning().walk_device) {
       rc = device_walk_batch(c, pool, threads, cs, n, flags, kind, seeded, head, job, out16,
                              out32, trace);
-      if (rc != kFallback) return rc;
-    }
-    if (!g_regions.empty() && kind != kWalkNone && tuning().span_fast) {
-      rc = span_fast_batch(c, n, flags, kind, seeded, head, job, out16, out32);
       if (rc != kFallback) return rc;
     }
     if (!g_regions.empty()) {

@@ -25,14 +25,15 @@
 //     of 16-byte chunks (the k_chains_pipe chunk list, cksum_chains.hip:
 //     segment lookup by LDS start markers + a DPP max-scan, 17x17 LDS mask
 //     table, telescoping DPP prefix sums into LDS bins), binned per
-//     (lane, logical parity); a segment of 2 KiB or more is streamed by the
-//     whole wave on its own;
+//     (lane, logical parity); the round's segments of 2 KiB or more are
+//     streamed by the whole wave, one after another, the next one's loads
+//     issued before this one's are summed;
 //   * a lane whose chain ends writes its result and takes the next packet of
 //     the wave's range at once (its job -- head, len, skip, seed -- was
 //     prefetched when it took the previous one), so every lane stays busy
 //     until the range runs dry: the rounds a wave runs are the range's mbufs
 //     / 64, not the longest chain times the packets per lane.  The range is
-//     handed out longest packet first (per window of 256 packets, by len), so
+//     handed out longest packet first (per window of 64 packets, by len), so
 //     the last rounds are short chains.
 // Every m_next hop costs one round trip, but 64 chains per wave and every
 // wave of the chip in flight keep ~100 K hops outstanding: the walk runs at

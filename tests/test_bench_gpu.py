@@ -107,14 +107,13 @@ def test_bench_nccl_world1_rccl_gather(tmp_path, torch_dev):
 def test_bench_n1_host_resident_cpu_line(torch_dev):
     """The N = 1 line folds its batch once more as host mbufs in registered
     memory and reports the host CPU that cost, beside the reference's
-    one-thread pass; bit-identical to the timed step.  With the mbufs
-    registered the GPU walks them; with only the bytes registered one mbuf
-    per packet takes the single-mbuf span path."""
+    one-thread pass; bit-identical to the timed step.  One mbuf per packet
+    takes the single-mbuf span path, with the mbufs registered or not."""
     d = _bench([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--packets", "65536"],
                {}, timeout=300)
     h = d["host_resident_cpu"]
     assert "error" not in h, h
-    assert h["bit_identical"] is True and h["path"] == "device walk"
+    assert h["bit_identical"] is True and h["path"] == "single-mbuf spans"
     b = h["bytes_only"]
     assert b["bit_identical"] is True and b["path"] == "single-mbuf spans"
     assert b["wall_ms"] > 0 and b["host_cpu_us_per_1k_pkts"] > 0

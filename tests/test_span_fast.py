@@ -22,17 +22,11 @@ pytestmark = pytest.mark.gpu
 
 @contextlib.contextmanager
 def registered(*bufs):
-    """`bufs` registered.  With the mbufs registered too the device walk
-    would take the batch first, so it is off inside (the span path then runs
-    with wide descriptors: the regions lie more than 4 GiB apart)."""
     for b in bufs:
         u.register_host(b)
-    if len(bufs) > 1:
-        u.set_tuning("walk_device", 0)
     try:
         yield
     finally:
-        u.set_tuning("walk_device", 1)
         for b in bufs:
             u.unregister_host(b)
 
@@ -60,7 +54,9 @@ def test_span_path_skip_batch(ora, arena, mbufs_registered):
     """One mbuf per packet at random offsets (odd addresses included), len
     short of / equal to / beyond the mbuf, skip inside / at / past its end,
     len <= skip, empty mbufs; with only the bytes or also the mbufs
-    registered (the span path needs only the bytes; the device walk off)."""
+    registered (the span path needs only the bytes and runs before the device
+    walk; with the mbufs registered far from the bytes its descriptors are
+    packed relative to the largest region)."""
     rng = np.random.default_rng(11)
     n = 20000
     ch, ln = _one_mbuf(rng, arena, n)
@@ -126,9 +122,10 @@ def test_span_path_pseudo_header(ora, arena):
         np.testing.assert_array_equal(got, want)
 
 
-def test_span_path_declines_long_and_unregistered(ora, arena):
-    """A piece over 65,535 B (the packed descriptor's limit) or a byte
-    outside the registered regions: the general path, same results."""
+def test_span_path_long_pieces_and_unregistered(ora, arena):
+    """A piece over 65,535 B (the packed descriptor's limit) sends the batch
+    round again with wide descriptors, still as spans; a byte outside the
+    registered regions sends it to the general path.  Same results."""
     rng = np.random.default_rng(14)
     n = 600
     big = rand_arena(1 << 20, 15)
@@ -139,7 +136,7 @@ def test_span_path_declines_long_and_unregistered(ora, arena):
     want = ora.skip_batch(ch.heads, ln, 0)
     with registered(arena):
         got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, ln, 0))
-    assert ns == 0
+    assert ns == 1
     np.testing.assert_array_equal(got, want)
     ch2 = MbufChains.contiguous(big, rng.integers(0, big.size - 1501, n), ln.clip(0, 1500))
     want2 = ora.skip_batch(ch2.heads, 1500, 0)
@@ -150,12 +147,30 @@ def test_span_path_declines_long_and_unregistered(ora, arena):
 
 
 def test_span_path_many_groups(ora, arena):
-    """A batch of several pipeline groups (64 K packets each), ragged tail."""
+    """A batch of several pipeline groups (64 K packets each), ragged tail,
+    the mbufs registered too (the span path still comes first)."""
     rng = np.random.default_rng(16)
     n = 3 * 65536 + 777
     ch, ln = _one_mbuf(rng, arena, n, max_len=1600)
     want = ora.skip_batch(ch.heads, ln, 0)
     with registered(arena, ch.mbufs):
         got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, ln, 0))
+    assert ns == 1
+    np.testing.assert_array_equal(got, want)
+
+
+def test_span_path_retries_wide_after_launched_groups(ora, arena):
+    """A piece over 65,535 B in the third pipeline group: the first two groups
+    were already folded with packed descriptors when the batch goes round
+    again with wide ones; every result is the wide round's."""
+    rng = np.random.default_rng(17)
+    n = 2 * 65536 + 1000
+    off = rng.integers(0, arena.size - 70001, n)
+    ln = rng.integers(0, 1501, n)
+    ln[2 * 65536 + 500] = 70000
+    ch = MbufChains.contiguous(arena, off, ln)
+    want = ora.skip_batch(ch.heads, ln, 3)
+    with registered(arena, ch.mbufs):
+        got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, ln, 3))
     assert ns == 1
     np.testing.assert_array_equal(got, want)
