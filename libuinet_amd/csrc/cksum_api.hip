@@ -929,7 +929,9 @@ int device_walk_batch(Ctx& c, HostPool& pool, int threads, int cs, int n, uint32
 // registered regions, or that is outside the reference's contract; the
 // caller then takes the general paths.  Called with g_reg_mu held (shared)
 // and at least one region registered.
-constexpr int kSpanGroup = 1 << 16;  // packets per pipeline group
+// Packets per pipeline group (16 K: 7 % slower; 256 K: the same;
+// profiles/r06/r06sab/).
+constexpr int kSpanGroup = 1 << 16;
 // Head mbufs are requested this many packets ahead.  One host thread spends
 // ~3 ns per packet and a head mbuf (a DRAM line, often on a page not touched
 // yet) takes ~100-300 ns to arrive, so the distance must cover ~100 packets:
@@ -1050,16 +1052,18 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
       }
       const uint32_t* dsd = seeded ? reinterpret_cast<const uint32_t*>(d + o_sd) : nullptr;
       const uint32_t hint = ng ? (uint32_t)(gb / (uint64_t)ng) : 0u;
+      // the bytes are read over PCIe: temporal loads (kFlagHostBytes)
+      const uint32_t fl = flags | kFlagHostBytes;
       if (packed)
         rc = launch_spans32(reinterpret_cast<const void*>(base),
                             reinterpret_cast<const uint32_t*>(d),
                             reinterpret_cast<const uint16_t*>(d + o_len), dsd, nullptr,
-                            static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags, hint, c.stream);
+                            static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, fl, hint, c.stream);
       else
         rc = launch_spans(reinterpret_cast<const void*>(base),
                           reinterpret_cast<const uint64_t*>(d),
                           reinterpret_cast<const uint32_t*>(d + o_len), dsd, nullptr,
-                          static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, flags, hint, c.stream);
+                          static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, fl, hint, c.stream);
       if (rc) {
         (void)ctx_wait(c);
         return rc;
@@ -1571,7 +1575,7 @@ int uinet_cksum_spans(const void* base, const uint64_t* off, const uint32_t* len
   if (n == 0) return UINET_CKSUM_OK;
   if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
   if (!base || !off || !len || !out) return UINET_CKSUM_EINVAL;
-  return launch_spans(base, off, len, seed, parity, out, n, flags, len_hint,
+  return launch_spans(base, off, len, seed, parity, out, n, flags & ~kFlagHostBytes, len_hint,
                       static_cast<hipStream_t>(stream));
 }
 
@@ -1581,7 +1585,7 @@ int uinet_cksum_spans32(const void* base, const uint32_t* off, const uint16_t* l
   if (n == 0) return UINET_CKSUM_OK;
   if (n > UINET_CKSUM_MAX_PACKETS) return UINET_CKSUM_EINVAL;
   if (!base || !off || !len || !out) return UINET_CKSUM_EINVAL;
-  return launch_spans32(base, off, len, seed, parity, out, n, flags, len_hint,
+  return launch_spans32(base, off, len, seed, parity, out, n, flags & ~kFlagHostBytes, len_hint,
                         static_cast<hipStream_t>(stream));
 }
 

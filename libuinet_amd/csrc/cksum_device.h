@@ -142,6 +142,13 @@ struct MaskLut {
 __device__ __forceinline__ u32x4 load_chunk(const uint8_t* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
+// kTemporal: an ordinary load (lines stay in L2 for the next reader), else
+// load_chunk's non-temporal one.
+template <bool kTemporal>
+__device__ __forceinline__ u32x4 load_chunk_t(const uint8_t* p) {
+  if constexpr (kTemporal) return *reinterpret_cast<const u32x4*>(p);
+  return load_chunk(p);
+}
 
 // One span [a, a + len) seen by the G lanes of a group, in rounds of G*U
 // chunks; chunk k (relative to the 16-B aligned-down start c0) belongs to

@@ -58,13 +58,18 @@ int launch_spans32(const void* base, const uint32_t* off, const uint16_t* len,
 // k_spans_lean (cksum_spans.hip): G = 32 or 64 lanes per packet; strided
 // takes packet i at base + i * stride, slen bytes (off / len unused, wide
 // descriptor types only); blocks_cu 0 = two steps per wave, else at most
-// blocks_cu blocks per CU.  Instantiated for (uint64_t, uint32_t) and
-// (uint32_t, uint16_t) descriptors.
+// blocks_cu blocks per CU; temporal: ordinary packet loads (no parity
+// array, not strided), for bytes read over PCIe.  Instantiated for
+// (uint64_t, uint32_t) and (uint32_t, uint16_t) descriptors.
 template <typename OffT, typename LenT>
 int launch_spans_lean(const void* base, const OffT* off, const LenT* len,
                       const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                       uint32_t flags, int g, int u, bool strided, uint64_t stride, uint32_t slen,
-                      int blocks_cu, hipStream_t stream);
+                      int blocks_cu, hipStream_t stream, bool temporal = false);
+// Internal flag bit for launch_spans / launch_spans32 (never a UINET_CKSUM_F_*
+// value; the public entry points clear it): the packet bytes lie in
+// registered host memory, read over PCIe.
+constexpr uint32_t kFlagHostBytes = 0x80000000u;
 // k_spans_quad (cksum_spans.hip): 4 lanes per packet, U = 1 or 2 chunk
 // slots per lane, for small packets.  Same instantiations.
 template <typename OffT, typename LenT>

@@ -161,13 +161,15 @@ static int launch_spans_t(const void* base, const OffT* off, const LenT* len,
                           const uint32_t* seed, const uint8_t* parity, uint16_t* out, uint32_t n,
                           uint32_t flags, uint32_t len_hint, hipStream_t stream) {
   if (n == 0) return UINET_CKSUM_OK;
+  const bool host_bytes = (flags & kFlagHostBytes) != 0;
+  flags &= ~kFlagHostBytes;
   const Geometry geo = pick_geometry(len_hint);
   if (geo.g == 4)
     return launch_spans_quad(base, off, len, seed, parity, out, n, flags, geo.u, false, 0, 0,
                              blocks_per_cu(128), stream);
   if (geo.g >= 32)
     return launch_spans_lean(base, off, len, seed, parity, out, n, flags, geo.g, geo.u, false, 0,
-                             0, tuning().blocks_per_cu, stream);
+                             0, tuning().blocks_per_cu, stream, host_bytes);
   const int grid = grid_for(n, geo.g, 256);
 #define L(G, U)                                                                          \
   UINET_LAUNCH((k_spans<G, U, false, OffT, LenT>), dim3(grid), dim3(kBlock), 0, stream,  \

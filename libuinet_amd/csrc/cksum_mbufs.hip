@@ -571,6 +571,8 @@ int launch_mbufs_xlate(const uint64_t* heads, const int32_t* len, const int32_t*
                        uint16_t* out, uint32_t n, uint32_t flags, uint32_t* status,
                        hipStream_t stream) {
   if (nreg < 1 || nreg > kWalkRegionsMax) return UINET_CKSUM_EINVAL;
+  // non-temporal: temporal loads measured 0-4 % slower on the hooks
+  // (profiles/r06/r06hostt/)
   return launch_mbufs_t<true, false>(heads, len, skip, seed, out, n, flags, regions, nreg,
                                      pseudo, status, stream);
 }

@@ -134,7 +134,7 @@ def test_fuzz_device_entry_points(ora):
             u.set_tuning(k, v)
 
 
-HOST_DEFAULTS = {"host_threads": min(16, os.cpu_count() or 1), "walk_device": 1}
+HOST_DEFAULTS = {"host_threads": min(16, os.cpu_count() or 1), "walk_device": 1, "span_fast": 1}
 
 
 def _host_trial(ora, arena, t):
@@ -143,8 +143,11 @@ def _host_trial(ora, arena, t):
     rng = np.random.default_rng(70000 + BASE + t)
     u.set_tuning("host_threads", int(rng.choice([1, 2, 5, 16])))
     u.set_tuning("walk_device", int(rng.integers(0, 4)))
-    n = int(rng.choice([1, 7, 64, int(rng.integers(1, 2500))]))
+    u.set_tuning("span_fast", int(rng.random() < 0.8))
+    n = int(rng.choice([1, 7, 64, 200, int(rng.integers(1, 2500))]))
     nseg = rng.integers(1, int(rng.choice([2, 6, 30])) + 1, n)  # a chain is >= 1 mbuf
+    if rng.random() < 0.3:  # one mbuf per packet: the single-mbuf span path's shape
+        nseg[:] = 1
     pkt_seg = np.concatenate([[0], np.cumsum(nseg)]).astype(np.int64)
     s = int(pkt_seg[-1])
     seg_len = _lengths(rng, s)
