@@ -532,10 +532,6 @@ def cpu_baseline(cfg: str, w, gpu_out, threads: int, keep=None):
         "host_read_ceiling_gibs": ceiling or None,
         "fastest_pass_gibs": fastest,
         "within_read_ceiling": (fastest <= ceiling) if ceiling else None,
-        # the same per (threads, placement), medians against medians: robust
-        # to the one lucky pass a floating placement sometimes gets
-        "medians_within_read": (all(rates[k] <= read_gibs[k] for k in rates if k in read_gibs)
-                                if read_gibs else None),
         "bit_identical_to_gpu": parity,
     }
 
