@@ -440,6 +440,9 @@ struct uinet_cksum_host_cpu {
 	uint64_t device_walks;   /* calls whose mbuf chains the GPU walked */
 	uint64_t span_batches;   /* calls folded as single-mbuf spans: the host read
 	                            each head mbuf, the GPU the bytes (no walk) */
+	uint64_t span_dma_bytes; /* bytes those calls moved to HBM by DMA copies
+	                            of dense packet ranges (the rest the GPU read
+	                            in place over PCIe) */
 };
 
 /* Copies the calling thread's counters to *st (may be NULL) and, when reset

@@ -497,7 +497,8 @@ class HostCpu(ctypes.Structure):
     """struct uinet_cksum_host_cpu (include/uinet_cksum.h section 2f)."""
 
     _fields_ = [("calls", _u64), ("packets", _u64), ("wall_ns", _u64), ("caller_cpu_ns", _u64),
-                ("helper_cpu_ns", _u64), ("device_walks", _u64), ("span_batches", _u64)]
+                ("helper_cpu_ns", _u64), ("device_walks", _u64), ("span_batches", _u64),
+                ("span_dma_bytes", _u64)]
 
 
 def host_cpu(reset: bool = False) -> dict:

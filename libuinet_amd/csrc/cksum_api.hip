@@ -159,7 +159,10 @@ CpuScope::~CpuScope() {
 }
 
 void note_device_walk() { t_cpu.device_walks++; }
-void note_span_fast() { t_cpu.span_batches++; }
+void note_span_fast(uint64_t dma) {
+  t_cpu.span_batches++;
+  t_cpu.span_dma_bytes += dma;
+}
 
 namespace {
 
@@ -186,6 +189,8 @@ struct Ctx {
   hipStream_t side = nullptr;  // device walk: the second stream of the walk/fold pipeline
   hipEvent_t fork = nullptr, join = nullptr;
   uint32_t walk_k = 0;        // device walk: segment slots per packet last needed
+  uint8_t* d_stage = nullptr;  // span path: HBM copy of a group's packet range
+  size_t stage_cap = 0;
 };
 
 // One context per (thread, device): a thread that serves several devices --
@@ -230,7 +235,11 @@ int ctx_current(Ctx** out) {
 // The lab build -DUINET_WAIT_SPIN waits in hipEventSynchronize instead (the
 // CPU-time A/B in DESIGN.md).
 constexpr long kSpinUs = 50;
-int ctx_wait(Ctx& c) {
+// `min_us`: a lower bound on the time the queued work still takes (0 =
+// unknown): the thread sleeps that long in one nap before it starts polling,
+// instead of the ~150 polls -- each a wakeup -- the geometric schedule below
+// spends over a 30-ms batch.
+int ctx_wait(Ctx& c, long min_us = 0) {
   int rc = record_hip(hipEventRecord(c.done, c.stream));
   if (rc) return rc;
 #ifdef UINET_WAIT_SPIN
@@ -239,6 +248,10 @@ int ctx_wait(Ctx& c) {
   using clk = std::chrono::steady_clock;
   const clk::time_point t0 = clk::now();
   int slack = -1;  // the thread's timer slack, restored on return
+  if (min_us > kSpinUs) {
+    const timespec ts{min_us / 1000000, (min_us % 1000000) * 1000};
+    nanosleep(&ts, nullptr);
+  }
   for (;;) {
     const hipError_t e = hipEventQuery(c.done);
     if (e != hipErrorNotReady) {
@@ -938,6 +951,8 @@ constexpr int kSpanGroup = 1 << 16;
 // config 2, one thread, host CPU per 1,000 packets at distance 8 / 32 / 64 /
 // 128 / 192: 6.3-6.8 / 4.4 / 3.4 / 2.8 / 2.8 us (profiles/r06/r06pf*/).
 constexpr int kSpanPrefetch = 128;
+// Groups summing fewer bytes are folded in place (a copy's fixed cost).
+constexpr uint64_t kSpanDmaMin = 1u << 20;
 template <typename HeadFn, typename JobFn>
 int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, const HeadFn& head,
                     const JobFn& job, uint16_t* out16, unsigned* out32) {
@@ -978,6 +993,8 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
     if (rc) return rc;
     const std::vector<Region>& regs = g_regions;
     bool bad = false;
+    uint64_t dma_bytes = 0, link_bytes = 0;  // link_bytes: what crosses PCIe, at least
+    std::chrono::steady_clock::time_point t_first;  // the first group's launch
     for (int g = 0; g < groups && !bad && !outside; g++) {
       const int i0 = g * G, ng = std::min(G, n - i0);
       uint8_t* h = c.h_buf + need * (size_t)g;
@@ -991,6 +1008,17 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
       // pass over it, so helpers would only add CPU time.
       uint64_t gb = 0;  // the group's summed bytes: its mean span picks the geometry
       const Region* last = nullptr;
+      // Offsets are relative to the group's origin `gbase` (its first span's
+      // address, 256-B aligned within its region), so that a dense group can
+      // be copied to HBM as one run with its descriptors as they are; a span
+      // before the origin sends the group's offsets back to the batch's base.
+      // The span kernel may read its base itself (an empty pair's offset is
+      // 0), and gbase is registered memory, as is base.
+      const uint64_t window = packed ? 0x100000000ull : ~0ull;
+      uint64_t gbase = 0, g_hi = 0;
+      bool local = false, has_gbase = false;
+      const Region* g_reg = nullptr;  // gbase's region
+      bool one_reg = true;
       const int e = i0 + ng;
       for (int i = i0; i < e; i++) {
         if (i + kSpanPrefetch < e) {
@@ -1024,13 +1052,49 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
               bad = true;
               break;
             }
-            if (span > (long)max_span || dev < base ||
-                dev - base + (uint64_t)span > 0x100000000ull) {
-              outside = true;  // packed only: wide descriptors take any of these
+            if (span > (long)max_span) {
+              outside = true;  // packed only: wide descriptors take it
               break;
             }
-            off = dev - base;
+            if (!has_gbase) {
+              has_gbase = local = true;
+              g_reg = last;
+              gbase = std::max(dev & ~uint64_t(255), (uint64_t)(last->base + last->delta));
+            }
+            if (local && (dev < gbase || dev - gbase + (uint64_t)span > window)) {
+              // back to the batch's base: the group's earlier offsets move
+              if (gbase < base) {
+                outside = true;
+                break;
+              }
+              const uint64_t sh = gbase - base;
+              for (int k = i0; k < i; k++) {
+                const bool nz = packed ? sl[k - i0] != 0 : wl[k - i0] != 0;
+                if (!nz) continue;
+                const uint64_t o = (packed ? (uint64_t)so[k - i0] : wo[k - i0]) + sh;
+                const uint64_t l = packed ? (uint64_t)sl[k - i0] : (uint64_t)wl[k - i0];
+                if (o + l > window) {
+                  outside = true;
+                  break;
+                }
+                if (packed) so[k - i0] = (uint32_t)o;
+                else wo[k - i0] = o;
+              }
+              if (outside) break;
+              local = false;
+            }
+            if (local) {
+              off = dev - gbase;
+            } else {
+              if (dev < base || dev - base + (uint64_t)span > window) {
+                outside = true;
+                break;
+              }
+              off = dev - base;
+            }
             len = (uint32_t)span;
+            g_hi = std::max(g_hi, dev + (uint64_t)span);
+            one_reg &= last == g_reg;
           }
         }
         if (packed) {
@@ -1044,6 +1108,49 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
         gb += len;
       }
       if (bad || outside) break;
+      // A dense group (its bytes one run of a region, at most 1/16 of it
+      // between packets: config 2, netmap rings of full frames) goes to HBM by
+      // one DMA copy and is folded there: the copy engines move 57.6 GB/s
+      // over the link where the span kernel's own reads of host memory get
+      // 48-52 (profiles/r06/).  The copy keeps every byte's address mod 256,
+      // so chunks and parities are the same; the kernel's base moves so that
+      // the descriptors written above address the copy.
+      uint64_t kbase = local ? gbase : base;
+      uint32_t fl = flags | kFlagHostBytes;  // read over PCIe: temporal loads
+      if (local && one_reg && gb >= kSpanDmaMin) {
+        const uint64_t lo_copy = gbase;
+        const uint64_t range = g_hi - lo_copy;
+        if (range <= gb + gb / 16 + 4096) {
+          // 256 B of headroom: a span's first chunk may start up to 15 B
+          // before the copy's first byte (masked, but loaded)
+          const size_t want = (size_t)range + 1024;
+          if (want > c.stage_cap) {  // grown between groups: drain what may read it
+            rc = ctx_wait(c);
+            if (rc) return rc;
+            if (c.d_stage) (void)hipFree(c.d_stage);
+            c.d_stage = nullptr;
+            c.stage_cap = 0;
+            size_t cap = std::max<size_t>(want, size_t(64) << 20);
+            rc = record_hip(hipMalloc((void**)&c.d_stage, cap));
+            if (rc) return rc;
+            c.stage_cap = cap;
+          }
+          uint8_t* dst = c.d_stage + 256 + (lo_copy & 255);
+          // (from the device alias as a device-to-device or default-kind
+          // copy: the same time and host CPU, profiles/r06/r06dma/)
+          rc = record_hip(hipMemcpyAsync(dst, reinterpret_cast<const void*>(lo_copy - g_reg->delta),
+                                         (size_t)range, hipMemcpyHostToDevice, c.stream));
+          if (rc) {
+            (void)ctx_wait(c);
+            return rc;
+          }
+          // the offsets (from gbase) now address the copy
+          kbase = reinterpret_cast<uint64_t>(dst);
+          fl = flags;  // HBM: non-temporal loads
+          dma_bytes += range;
+          link_bytes += range - gb;  // gb is added below
+        }
+      }
       uint8_t* d = c.d_buf + need * (size_t)g;
       rc = record_hip(hipMemcpyAsync(d, h, need, hipMemcpyHostToDevice, c.stream));
       if (rc) {
@@ -1052,15 +1159,13 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
       }
       const uint32_t* dsd = seeded ? reinterpret_cast<const uint32_t*>(d + o_sd) : nullptr;
       const uint32_t hint = ng ? (uint32_t)(gb / (uint64_t)ng) : 0u;
-      // the bytes are read over PCIe: temporal loads (kFlagHostBytes)
-      const uint32_t fl = flags | kFlagHostBytes;
       if (packed)
-        rc = launch_spans32(reinterpret_cast<const void*>(base),
+        rc = launch_spans32(reinterpret_cast<const void*>(kbase),
                             reinterpret_cast<const uint32_t*>(d),
                             reinterpret_cast<const uint16_t*>(d + o_len), dsd, nullptr,
                             static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, fl, hint, c.stream);
       else
-        rc = launch_spans(reinterpret_cast<const void*>(base),
+        rc = launch_spans(reinterpret_cast<const void*>(kbase),
                           reinterpret_cast<const uint64_t*>(d),
                           reinterpret_cast<const uint32_t*>(d + o_len), dsd, nullptr,
                           static_cast<uint16_t*>(dout) + i0, (uint32_t)ng, fl, hint, c.stream);
@@ -1068,13 +1173,25 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
         (void)ctx_wait(c);
         return rc;
       }
+      link_bytes += gb;
+      if (g == 0) t_first = std::chrono::steady_clock::now();
     }
-    rc = ctx_wait(c);  // the groups launched so far (their buffers are reused)
+    // The GPU cannot have moved the bytes over the link faster than 64 GB/s
+    // (PCIe 5.0 x16; the copy engines reach 57.6 here) since the first launch:
+    // that lower bound is slept in one nap.
+    long min_us = 0;
+    if (!bad && !outside && link_bytes > 0) {
+      const long since = (long)std::chrono::duration_cast<std::chrono::microseconds>(
+                             std::chrono::steady_clock::now() - t_first)
+                             .count();
+      min_us = std::max(0l, (long)(link_bytes / 64000u) - since);
+    }
+    rc = ctx_wait(c, min_us);  // the groups launched so far (their buffers are reused)
     if (rc) return rc;
     if (bad) return kFallback;
     if (outside) continue;
     deliver(c, n, out16, out32);
-    note_span_fast();
+    note_span_fast(dma_bytes);
     return UINET_CKSUM_OK;
   }
   return kFallback;

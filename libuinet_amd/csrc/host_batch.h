@@ -92,8 +92,9 @@ struct CpuScope {
 };
 // The calling thread's batch was walked on the device (counted by the scope).
 void note_device_walk();
-// The calling thread's batch went down the single-mbuf span path.
-void note_span_fast();
+// The calling thread's batch went down the single-mbuf span path, `dma`
+// bytes of it copied to HBM by DMA.
+void note_span_fast(uint64_t dma);
 
 // The per-call ABI's host fold (cksum_percall.cpp): one chain on the calling
 // thread, no device involved, no error path (like the reference).

@@ -174,3 +174,64 @@ def test_span_path_retries_wide_after_launched_groups(ora, arena):
         got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, ln, 3))
     assert ns == 1
     np.testing.assert_array_equal(got, want)
+
+
+def test_span_path_dense_groups_copy_to_hbm(ora):
+    """Packets back to back in one registered region (config 2's layout, at
+    odd and even starts, empty and short packets among them): each pipeline
+    group's byte range goes to HBM by one DMA copy and is folded there
+    (host_cpu()["span_dma_bytes"]; groups under 1 MiB are read in place);
+    results equal the oracle.  The same
+    packets spread out (gaps over 1/16 of the bytes) are read in place."""
+    rng = np.random.default_rng(18)
+    n = 2 * 65536 + 333
+    ln = rng.integers(600, 1501, n)
+    ln[rng.random(n) < 0.01] = 0
+    ln[rng.random(n) < 0.01] = 1
+    off = 3 + np.concatenate([[0], np.cumsum(ln)[:-1]])
+    arena = rand_arena(int(off[-1] + ln[-1] + 64), 19)
+    ch = MbufChains.contiguous(arena, off, ln)
+    skip = rng.integers(0, 3, n)
+    want = ora.skip_batch(ch.heads, ln, skip)
+    before = u.host_cpu()["span_dma_bytes"]
+    with registered(arena, ch.mbufs):
+        got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, ln, skip))
+    moved = u.host_cpu()["span_dma_bytes"] - before
+    assert ns == 1
+    np.testing.assert_array_equal(got, want)
+    # the two full groups (64 K packets each) by DMA; the 333-packet tail
+    # (under 1 MiB) in place
+    summed = ln - np.minimum(skip, ln)
+    assert int(summed[:2 * 65536].sum()) <= moved <= int(summed.sum()) + 3 * 4096
+    # spread: every packet followed by a gap of its own length
+    off2 = 5 + np.concatenate([[0], np.cumsum(2 * ln)[:-1]])
+    arena2 = rand_arena(int(off2[-1] + ln[-1] + 64), 20)
+    ch2 = MbufChains.contiguous(arena2, off2, ln)
+    want2 = ora.skip_batch(ch2.heads, ln, skip)
+    before = u.host_cpu()["span_dma_bytes"]
+    with registered(arena2):
+        got2, ns2 = spans(lambda: u.in_cksum_skip_batch(ch2.heads, ln, skip))
+    assert ns2 == 1 and u.host_cpu()["span_dma_bytes"] == before
+    np.testing.assert_array_equal(got2, want2)
+
+
+def test_span_path_dense_pseudo_header(ora):
+    """The pseudo-header form over a dense layout (config 5's jumbo frames
+    back to back): DMA copies, seeds, results equal the oracle."""
+    rng = np.random.default_rng(21)
+    n = 40000
+    ln = np.full(n, 9000)
+    off = np.arange(n, dtype=np.int64) * 9000
+    arena = rand_arena(int(off[-1] + 9000 + 64), 22)
+    ch = MbufChains.contiguous(arena, off, ln)
+    off0 = np.full(n, 20)
+    plen = ln - 20
+    src, dst = (rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) for _ in range(2))
+    proto = rng.choice(np.array([6, 17], np.uint8), n)
+    want = ora.pseudo_header_batch(ch.heads, plen, off0, src, dst, proto)
+    before = u.host_cpu()["span_dma_bytes"]
+    with registered(arena):
+        got, ns = spans(lambda: u.in_cksum_pseudo_header_batch(ch.heads, plen, off0, src, dst,
+                                                                proto))
+    assert ns == 1 and u.host_cpu()["span_dma_bytes"] > before
+    np.testing.assert_array_equal(got, want)

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-r06b3}; mkdir -p $O
-for r in 1 2 3; do
+for r in ${RUNS:-1 2 3}; do
   timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench$r.json 2> $O/bench$r.err || { tail -20 $O/bench$r.err; exit 1; }
   python -c "
 import json;d=json.load(open('$O/bench$r.json'));c=d['cpu_baseline'];h=d['host_resident_cpu']
