@@ -1021,7 +1021,7 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
       bool one_reg = true;
       const int e = i0 + ng;
       for (int i = i0; i < e; i++) {
-        if (i + kSpanPrefetch < e) {
+        if (i + kSpanPrefetch < e) {  // (the locality hint makes no difference, r06pfab/)
           const auto r = head(i + kSpanPrefetch);
           if (r.m) __builtin_prefetch(r.m, 0, 3);
         }
