@@ -995,6 +995,11 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
     bool bad = false;
     uint64_t dma_bytes = 0, link_bytes = 0;  // link_bytes: what crosses PCIe, at least
     std::chrono::steady_clock::time_point t_first;  // the first group's launch
+    // UINET_CKSUM_TRACE_HOST=1: where the calling thread's time goes (tools)
+    static const bool trace = getenv("UINET_CKSUM_TRACE_HOST") != nullptr;
+    using tclk = std::chrono::steady_clock;
+    const tclk::time_point t_in = trace ? tclk::now() : tclk::time_point();
+    double pass_us = 0;
     for (int g = 0; g < groups && !bad && !outside; g++) {
       const int i0 = g * G, ng = std::min(G, n - i0);
       uint8_t* h = c.h_buf + need * (size_t)g;
@@ -1007,6 +1012,7 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
       // reads, and the GPU's fold of a group takes longer than the host's
       // pass over it, so helpers would only add CPU time.
       uint64_t gb = 0;  // the group's summed bytes: its mean span picks the geometry
+      const tclk::time_point t_g = trace ? tclk::now() : tclk::time_point();
       const Region* last = nullptr;
       // Offsets are relative to the group's origin `gbase` (its first span's
       // address, 256-B aligned within its region), so that a dense group can
@@ -1108,6 +1114,8 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
         gb += len;
       }
       if (bad || outside) break;
+      if (trace)
+        pass_us += std::chrono::duration<double, std::micro>(tclk::now() - t_g).count();
       // A dense group (its bytes one run of a region, at most 1/16 of it
       // between packets: config 2, netmap rings of full frames) goes to HBM by
       // one DMA copy and is folded there: the copy engines move 57.6 GB/s
@@ -1186,12 +1194,24 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
                              .count();
       min_us = std::max(0l, (long)(link_bytes / 64000u) - since);
     }
+    const tclk::time_point t_w = trace ? tclk::now() : tclk::time_point();
     rc = ctx_wait(c, min_us);  // the groups launched so far (their buffers are reused)
     if (rc) return rc;
     if (bad) return kFallback;
     if (outside) continue;
+    const tclk::time_point t_d = trace ? tclk::now() : tclk::time_point();
     deliver(c, n, out16, out32);
     note_span_fast(dma_bytes);
+    if (trace) {
+      const auto us = [](tclk::time_point a, tclk::time_point b) {
+        return std::chrono::duration<double, std::micro>(b - a).count();
+      };
+      fprintf(stderr,
+              "uinet_cksum spans: n=%d groups=%d dma %.1f MB | pass %.0f us, calls %.0f us, "
+              "wait %.0f us (slept %ld), deliver %.0f us, total %.0f us\n",
+              n, groups, dma_bytes / 1e6, pass_us, us(t_in, t_w) - pass_us, us(t_w, t_d), min_us,
+              us(t_d, tclk::now()), us(t_in, tclk::now()));
+    }
     return UINET_CKSUM_OK;
   }
   return kFallback;
