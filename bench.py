@@ -614,6 +614,11 @@ def host_offload_row(keep, bufs, n, nbytes, gpu_out, link, reps):
         "path": ("single-mbuf spans" if st["span_batches"] == st["calls"] else
                  "device walk" if st["device_walks"] == st["calls"] else "host walk"),
         "device_walked": bool(st["device_walks"] == st["calls"]),
+        # on the span path: whether the GPU read the head mbufs (mbufs
+        # registered) or the calling thread did
+        "heads_read_by": ("gpu" if st["device_walks"] == st["calls"] else "host")
+                         if st["span_batches"] == st["calls"] else None,
+        "dma_bytes": int(st.get("span_dma_bytes", 0)),
         "bit_identical": bool(all(np.array_equal(r[2], gpu_out) for r in rows)),
         # the link's own rate, measured here: one DMA copy of the same registered
         # bytes to HBM; the batch's summed bytes over its wall time against it

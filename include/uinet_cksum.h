@@ -164,8 +164,12 @@ int uinet_cksum_device_ok(void);
  *   "span_fast"       host-mbuf batches (2c, 2d) over registered packet bytes
  *                     whose every sum lies in the packet's first mbuf (one
  *                     mbuf per packet, the netmap RX shape): 1 (default) the
- *                     host reads each head mbuf and the GPU folds the bytes as
- *                     spans, no mbuf line crosses the link; 0 = the walks below
+ *                     calling thread reads each head mbuf and the GPU folds the
+ *                     bytes as spans, dense runs copied to HBM first, no mbuf
+ *                     line crosses the link; 2 = the same with the head mbufs
+ *                     read by the GPU when they are registered (less host CPU,
+ *                     one 128-B link line per packet more); 0 = the walks
+ *                     below
  *   "multi_gather"    uinet_cksum_spans_multi: 0 = one RCCL gather when it
  *                     applies (default), 1 = always peer copies
  * Returns UINET_CKSUM_OK, or UINET_CKSUM_EINVAL for an unknown key/value.

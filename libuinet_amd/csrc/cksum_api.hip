@@ -83,7 +83,7 @@ static std::atomic<int>* tuning_field(TuningLive& t, const char* key, int value)
       {"multi_gather", &TuningLive::multi_gather, [](int v) { return v == 0 || v == 1; }},
       {"walk_device", &TuningLive::walk_device, [](int v) { return v >= 0 && v <= 3; }},
       {"chains_wide", &TuningLive::chains_wide, [](int v) { return v >= 0 && v <= 2; }},
-      {"span_fast", &TuningLive::span_fast, [](int v) { return v == 0 || v == 1; }},
+      {"span_fast", &TuningLive::span_fast, [](int v) { return v >= 0 && v <= 2; }},
   };
   for (const Knob& k : knobs)
     if (!strcmp(key, k.key)) return k.ok(value) ? &(t.*k.field) : nullptr;
@@ -191,6 +191,7 @@ struct Ctx {
   uint32_t walk_k = 0;        // device walk: segment slots per packet last needed
   uint8_t* d_stage = nullptr;  // span path: HBM copy of a group's packet range
   size_t stage_cap = 0;
+  std::vector<hipEvent_t> gev;  // span walk: one event per group
 };
 
 // One context per (thread, device): a thread that serves several devices --
@@ -699,6 +700,15 @@ WalkWork walk_work(size_t N, uint32_t K) {
   return w;
 }
 
+// The context's side stream and its fork / join events, created on first use.
+int ctx_side(Ctx& c) {
+  int rc = UINET_CKSUM_OK;
+  if (!c.side) rc = record_hip(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+  if (!rc && !c.fork) rc = record_hip(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+  if (!rc && !c.join) rc = record_hip(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
+  return rc;
+}
+
 // Enqueues the walk (k_walk_mbufs) and the fold (k_chains_pipe) of N jobs --
 // device-readable arrays jm / jl / js / jd (jd may be NULL) -- over the work
 // area at `wa` (HBM), results into `out`, status bits into `dstatus` (zeroed
@@ -716,13 +726,8 @@ int launch_walk_fold(Ctx& c, const uint64_t* jm, const int32_t* jl, const int32_
 #endif
   const int n = (int)N;
   const int groups = n >= 2 * kWalkGroupMin ? std::min(UINET_WALK_GROUPS, n / kWalkGroupMin) : 1;
-  int rc = UINET_CKSUM_OK;
-  if (groups > 1 && !c.side) {
-    rc = record_hip(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-    if (!rc) rc = record_hip(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
-    if (!rc) rc = record_hip(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
-    if (rc) return rc;
-  }
+  int rc = groups > 1 ? ctx_side(c) : UINET_CKSUM_OK;
+  if (rc) return rc;
   const WalkWork W = walk_work(N, K);
   if (groups > 1) rc = record_hip(hipEventRecord(c.fork, c.stream));
   if (!rc && groups > 1) rc = record_hip(hipStreamWaitEvent(c.side, c.fork, 0));
@@ -1217,6 +1222,221 @@ int span_fast_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, c
   return kFallback;
 }
 
+// ---- single-mbuf spans, heads read by the GPU ------------------------------
+//
+// The span path above with the mbufs registered too: instead of the calling
+// thread reading every head mbuf (one DRAM line per packet, 2.7-3.9 us of CPU
+// per 1,000 packets by host), it copies the jobs (20 B per packet, sequential)
+// and the GPU reads the heads over PCIe (k_span_walk: one 128-B link line per
+// packet).  Per group of kSpanGroup packets, on the side stream: the walk, then
+// its stats to pinned memory; the calling thread waits for each group's stats
+// and then, on the main stream, copies a dense group to HBM as one run (as the
+// host span path does) or folds it in place, after rebasing its offsets.  The
+// walks run ahead on their stream while the copies of earlier groups use the
+// copy engines.  Returns kFallback (everything drained) when any packet is
+// not the shape; the caller then takes the other paths.  Called with
+// g_reg_mu held (shared).
+template <typename HeadFn, typename JobFn>
+int span_walk_batch(Ctx& c, int n, uint32_t flags, WalkKind kind, bool seeded, const HeadFn& head,
+                    const JobFn& job, uint16_t* out16, unsigned* out32) {
+  const size_t nreg_all = g_regions.size();
+  if (nreg_all == 0 || nreg_all > (size_t)kWalkRegionsMax) return kFallback;
+  if (!heads_registered(n, [&](int i) { return head(i).m; })) return kFallback;
+  // a quick look at three heads: a chain whose sum needs its second mbuf
+  // means the batch is not this shape (config 3), before anything is queued
+  {
+    const int idx[3] = {0, n / 2, n - 1};
+    for (int i : idx) {
+      const auto r = head(i);
+      if (r.m && r.m->m_next && r.limit > r.m->m_len) return kFallback;
+    }
+  }
+  using clk = std::chrono::steady_clock;
+  static const bool trace = getenv("UINET_CKSUM_TRACE_HOST") != nullptr;
+  const clk::time_point t_in = trace ? clk::now() : clk::time_point();
+  const auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const size_t N = (size_t)n;
+  const int G = std::min(n, kSpanGroup);
+  const int groups = (n + G - 1) / G;
+  // pinned: heads u64 | len i32 | skip i32 | seed u32 | regions | stats u64[6] x groups
+  //         | the stats' initial value u64[6]
+  const size_t h_len = a16(8 * N), h_skip = h_len + a16(4 * N), h_seed = h_skip + a16(4 * N);
+  const size_t h_reg = h_seed + (seeded ? a16(4 * N) : 0);
+  const size_t h_st = h_reg + a16(sizeof(WalkRegionHost) * nreg_all);
+  const size_t h_init = h_st + 48 * (size_t)groups, h_end = h_init + 48;
+  // HBM: off u64 | len u32 | seed u32 | stats u64[6] x groups
+  const size_t d_len = a16(8 * N), d_seed = d_len + a16(4 * N);
+  const size_t d_st = d_seed + (seeded ? a16(4 * N) : 0), d_end = d_st + 48 * (size_t)groups;
+  int rc = ctx_reserve(c, h_end, N, d_end);
+  if (rc) return rc;
+  rc = ctx_side(c);
+  if (rc) return rc;
+  while ((int)c.gev.size() < groups) {
+    hipEvent_t e;
+    rc = record_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (rc) return rc;
+    c.gev.push_back(e);
+  }
+  uint8_t* h = c.h_buf;
+  uint64_t* heads = reinterpret_cast<uint64_t*>(h);
+  int32_t* jl = reinterpret_cast<int32_t*>(h + h_len);
+  int32_t* js = reinterpret_cast<int32_t*>(h + h_skip);
+  uint32_t* jd = reinterpret_cast<uint32_t*>(h + h_seed);
+  for (int i = 0; i < n; i++) {  // the calling thread: 20 B per packet, in order
+    const Job J = job(i);
+    heads[i] = reinterpret_cast<uint64_t>(J.m);
+    jl[i] = J.len;
+    js[i] = J.skip;
+    if (seeded) jd[i] = J.seed;
+  }
+  size_t nreg = 0;
+  uint64_t lo_addr = 0;
+  (void)walk_regions(reinterpret_cast<WalkRegionHost*>(h + h_reg), nreg_all, &nreg, &lo_addr);
+  const WalkRegionHost* RH = reinterpret_cast<const WalkRegionHost*>(h + h_reg);
+  uint64_t* init = reinterpret_cast<uint64_t*>(h + h_init);
+  init[0] = ~0ull;
+  init[1] = init[2] = init[3] = 0;
+  init[4] = ~0ull;
+  init[5] = 0;
+  void* dh = nullptr;
+  rc = record_hip(hipHostGetDevicePointer(&dh, c.h_buf, 0));
+  if (rc) return rc;
+  void* dout = nullptr;
+  rc = record_hip(hipHostGetDevicePointer(&dout, c.h_out, 0));
+  if (rc) return rc;
+  const uint8_t* dj = static_cast<const uint8_t*>(dh);
+  uint8_t* d = c.d_buf;
+  uint64_t* doff = reinterpret_cast<uint64_t*>(d);
+  uint32_t* dlen = reinterpret_cast<uint32_t*>(d + d_len);
+  uint32_t* dsd = seeded ? reinterpret_cast<uint32_t*>(d + d_seed) : nullptr;
+  unsigned long long* dst_st = reinterpret_cast<unsigned long long*>(d + d_st);
+  volatile uint64_t* hst = reinterpret_cast<volatile uint64_t*>(h + h_st);
+  // the walks, all of them, on the side stream (after what c.stream holds)
+  rc = record_hip(hipEventRecord(c.gev[0], c.stream));
+  if (!rc) rc = record_hip(hipStreamWaitEvent(c.side, c.gev[0], 0));
+  for (int g = 0; g < groups && !rc; g++) {
+    const int i0 = g * G, ng = std::min(G, n - i0);
+    rc = record_hip(hipMemcpyAsync(dst_st + 6 * g, init, 48, hipMemcpyHostToDevice, c.side));
+    if (!rc)
+      rc = launch_span_walk(reinterpret_cast<const uint64_t*>(dj) + i0,
+                            reinterpret_cast<const int32_t*>(dj + h_len) + i0,
+                            reinterpret_cast<const int32_t*>(dj + h_skip) + i0,
+                            seeded ? reinterpret_cast<const uint32_t*>(dj + h_seed) + i0 : nullptr,
+                            reinterpret_cast<const WalkRegionHost*>(dj + h_reg), (int)nreg,
+                            (uint32_t)ng, kind == kWalkPseudo, doff + i0, dlen + i0,
+                            dsd ? dsd + i0 : nullptr, dst_st + 6 * g, c.side);
+    if (!rc)
+      rc = record_hip(hipMemcpyAsync(const_cast<uint64_t*>(hst) + 6 * g, dst_st + 6 * g, 48,
+                                     hipMemcpyDeviceToHost, c.side));
+    if (!rc) rc = record_hip(hipEventRecord(c.gev[g], c.side));
+  }
+  const auto drain = [&]() {
+    (void)hipStreamSynchronize(c.side);
+    (void)ctx_wait(c);
+  };
+  if (rc) {
+    drain();
+    return rc;
+  }
+  uint64_t dma_bytes = 0, link_bytes = 0;
+  clk::time_point t_first;
+  double wait_us = 0;
+  for (int g = 0; g < groups; g++) {
+    const int i0 = g * G, ng = std::min(G, n - i0);
+    // this group's walk: sleep-poll its event (a walk takes a few hundred us)
+    const clk::time_point tw = clk::now();
+    for (;;) {
+      const hipError_t e = hipEventQuery(c.gev[g]);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) {
+        drain();
+        return record_hip(e);
+      }
+      const long us = (long)std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - tw)
+                          .count();
+      const long nap = std::min(500l, std::max(20l, us / 8));
+      const timespec ts{0, nap * 1000};
+      nanosleep(&ts, nullptr);
+    }
+    if (trace) wait_us += std::chrono::duration<double, std::micro>(clk::now() - tw).count();
+    const uint64_t lo = hst[6 * g], hi = hst[6 * g + 1], gb = hst[6 * g + 2];
+    const uint64_t bad = hst[6 * g + 3], rmin = hst[6 * g + 4], rmax = hst[6 * g + 5];
+    if (bad) {  // not the shape (or outside the regions): the other paths
+      drain();
+      return kFallback;
+    }
+    // the group's origin: its lowest span's 256-B line within its region
+    // when one region holds it, else the lowest registered byte
+    uint64_t gbase = lo_addr;
+    const bool one = gb && rmin == rmax && rmin < nreg;
+    if (one) {
+      const uint64_t r_lo = RH[rmin].base + (uint64_t)RH[rmin].delta;
+      gbase = std::max(lo & ~uint64_t(255), r_lo);
+    }
+    rc = record_hip(hipStreamWaitEvent(c.stream, c.gev[g], 0));
+    uint64_t kbase = gbase;
+    uint32_t fl = flags | kFlagHostBytes;
+    if (!rc && one && gb >= kSpanDmaMin && hi - gbase <= gb + gb / 16 + 4096) {
+      const uint64_t range = hi - gbase;
+      const size_t want = (size_t)range + 1024;
+      if (want > c.stage_cap) {  // grown between groups: drain what may read it
+        rc = ctx_wait(c);
+        if (!rc) {
+          if (c.d_stage) (void)hipFree(c.d_stage);
+          c.d_stage = nullptr;
+          c.stage_cap = 0;
+          const size_t cap = std::max<size_t>(want, size_t(64) << 20);
+          rc = record_hip(hipMalloc((void**)&c.d_stage, cap));
+          if (!rc) c.stage_cap = cap;
+        }
+      }
+      if (!rc) {
+        uint8_t* dstp = c.d_stage + 256 + (gbase & 255);
+        rc = record_hip(hipMemcpyAsync(dstp, reinterpret_cast<const void*>(gbase - (uint64_t)RH[rmin].delta),
+                                       (size_t)range, hipMemcpyHostToDevice, c.stream));
+        kbase = reinterpret_cast<uint64_t>(dstp);
+        fl = flags;
+        dma_bytes += range;
+        link_bytes += range - gb;
+      }
+    }
+    if (!rc) rc = launch_span_rebase(doff + i0, dlen + i0, (uint32_t)ng, gbase, c.stream);
+    if (!rc)
+      rc = launch_spans(reinterpret_cast<const void*>(kbase), doff + i0, dlen + i0,
+                        dsd ? dsd + i0 : nullptr, nullptr, static_cast<uint16_t*>(dout) + i0,
+                        (uint32_t)ng, fl, ng ? (uint32_t)(gb / (uint64_t)ng) : 0u, c.stream);
+    if (rc) {
+      drain();
+      return rc;
+    }
+    link_bytes += gb;
+    if (g == 0) t_first = clk::now();
+  }
+  long min_us = 0;
+  if (link_bytes) {
+    const long since =
+        (long)std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t_first).count();
+    min_us = std::max(0l, (long)(link_bytes / 64000u) - since);
+  }
+  const clk::time_point t_w = trace ? clk::now() : clk::time_point();
+  rc = ctx_wait(c, min_us);
+  if (rc) {
+    (void)hipStreamSynchronize(c.side);
+    return rc;
+  }
+  deliver(c, n, out16, out32);
+  note_span_fast(dma_bytes);
+  note_device_walk();
+  if (trace)
+    fprintf(stderr,
+            "uinet_cksum spans (GPU-read heads): n=%d groups=%d dma %.1f MB | group waits %.0f "
+            "us, final wait %.0f us (slept %ld), total %.0f us\n",
+            n, groups, dma_bytes / 1e6, wait_us,
+            std::chrono::duration<double, std::micro>(clk::now() - t_w).count(), min_us,
+            std::chrono::duration<double, std::micro>(clk::now() - t_in).count());
+  return UINET_CKSUM_OK;
+}
+
 struct ChainRef {
   const MbufHdr* m;  // first mbuf, nullptr = nothing to chase
   long limit;        // bytes from the chain start the walk consumes
@@ -1329,6 +1549,14 @@ int run_host_batch(int n, uint32_t flags, uint16_t* out16, unsigned* out32, Walk
     // device walk when the mbufs are registered too, then the host walk
     // (profiles/r06/NOTES.md)
     if (!g_regions.empty() && kind != kWalkNone && tuning().span_fast) {
+      // span_fast 2: the GPU reads the head mbufs when they are registered
+      // (1.4 us of host CPU per 1,000 packets instead of ~3.4, but 0.81 of the
+      // link instead of 0.91: each head crosses it as a 128-B line,
+      // profiles/r06/r06q/)
+      if (tuning().span_fast == 2) {
+        rc = span_walk_batch(c, n, flags, kind, seeded, head, job, out16, out32);
+        if (rc != kFallback) return rc;
+      }
       rc = span_fast_batch(c, n, flags, kind, seeded, head, job, out16, out32);
       if (rc != kFallback) return rc;
     }

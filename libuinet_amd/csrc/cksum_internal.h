@@ -23,7 +23,8 @@ struct Tuning {
   int xcd_remap;       // span kernels: XCD-banded block order (0/1)
   int multi_gather;    // uinet_cksum_spans_multi: 0 RCCL gather when it applies, 1 peer copies
   int span_fast;       // host-mbuf batches whose sums lie in the first mbuf: 1 the host
-                       // writes span descriptors (no device walk), 0 off
+                       // reads the heads and writes span descriptors, 2 the GPU reads
+                       // the heads when the mbufs are registered, 0 off
   int walk_device;     // host-mbuf batches in registered memory, 0 the host walks them,
                        // else the GPU: 3 walks and folds in one launch (cksum_mbufs.hip),
                        // 2 walks into a segment list first (cksum_walk.hip), 1 = 2 for
@@ -111,6 +112,19 @@ int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* 
                       uint32_t K, uint32_t seg_base, uint64_t lo_dev, bool pseudo, uint64_t* seg_off,
                       uint32_t* seg_len, uint32_t* pkt_seg, uint32_t* len_out, uint32_t* skip_out,
                       uint32_t* seed_out, uint32_t* status, hipStream_t stream);
+
+// The single-mbuf span walk (cksum_walk.hip, k_span_walk): packet i's span
+// from its head mbuf, as a device address (off_out) and length, or status
+// bits in stats[3] when the batch is not that shape; stats (6 u64, set by the
+// caller to {~0, 0, 0, 0, ~0, 0}): lowest span address, highest span end,
+// summed bytes, status, lowest and highest region index.  launch_span_rebase:
+// off[i] -= gbase where len[i] != 0, else 0.
+int launch_span_walk(const uint64_t* heads, const int32_t* len, const int32_t* skip,
+                     const uint32_t* seed, const WalkRegionHost* regions, int nreg, uint32_t n,
+                     bool pseudo, uint64_t* off_out, uint32_t* len_out, uint32_t* seed_out,
+                     unsigned long long* stats, hipStream_t stream);
+int launch_span_rebase(uint64_t* off, const uint32_t* len, uint32_t n, uint64_t gbase,
+                       hipStream_t stream);
 
 // The fused mbuf walk + fold (cksum_mbufs.hip).  launch_mbufs: chains in
 // device memory (uinet_cksum_mbufs; status: UINET_CKSUM_MBUF_* bits).

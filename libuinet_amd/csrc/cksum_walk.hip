@@ -139,7 +139,136 @@ __global__ __launch_bounds__(256) void k_walk_mbufs(
   }
 }
 
+// One lane per packet: a batch whose every sum lies in its packet's first
+// mbuf (the single-mbuf span path with the mbufs registered too), read by the
+// GPU instead of the host.  Packet i's head mbuf (its first 32 bytes) gives the
+// span [m_data + skip, m_data + min(len, m_len)) exactly as the host span path
+// takes it (in_cksum.c:203-229, :254-272; cksum_api.hip span_fast_batch):
+// its device address and length go to off / len (0 / 0 when nothing is
+// summed), the seed to seed_out.  A sum that needs a second mbuf, a negative
+// skip or m_len, or a byte outside the regions sets status bits and the host
+// takes the batch another way.  stats (6 u64, initialised by the caller to
+// {~0, 0, 0, 0, ~0, 0}): the lowest span address, the highest span end, the
+// summed bytes, the status bits, the lowest and highest region index -- what
+// the host needs to copy a dense group to HBM in one run.
+__global__ __launch_bounds__(256) void k_span_walk(
+    const uint64_t* __restrict__ heads, const int32_t* __restrict__ jlen,
+    const int32_t* __restrict__ jskip, const uint32_t* __restrict__ jseed,
+    const WalkRegion* __restrict__ regions, int nreg, uint32_t n, int pseudo,
+    uint64_t* __restrict__ off_out, uint32_t* __restrict__ len_out,
+    uint32_t* __restrict__ seed_out, unsigned long long* __restrict__ stats) {
+  __shared__ WalkRegion R[kWalkRegionsMax];
+  for (int k = (int)threadIdx.x; k < nreg; k += (int)blockDim.x) R[k] = regions[k];
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t lo = ~0ull, hi = 0, bytes = 0;
+  uint32_t bad = 0, rmin = ~0u, rmax = 0;
+  if (i < n) {
+    const uint64_t m = heads[i];
+    const int32_t L = jlen[i], S = jskip[i];
+    uint64_t off = 0;
+    uint32_t len = 0;
+    if (S < 0) {
+      bad = kWalkFallback;
+    } else if (m && L > S) {
+      uint64_t dm;
+      if (!walk_xlate(R, nreg, m, 32, &dm)) {
+        bad = kWalkUnmapped;
+      } else {
+        // m_next, m_nextpkt | m_data, m_len, m_flags (sys/sys/mbuf.h:90-98)
+        const u32x4 a = reinterpret_cast<const GlobalU32x4*>(dm)[0];
+        const u32x4 b = reinterpret_cast<const GlobalU32x4*>(dm)[1];
+        const uint64_t next = (uint64_t)a.x | (uint64_t)a.y << 32;
+        const uint64_t data = (uint64_t)b.x | (uint64_t)b.y << 32;
+        const int32_t ml = (int32_t)b.z;
+        const bool more = next != 0;
+        const bool second = S < ml ? (L > ml && more) : (more || (pseudo && S > ml));
+        if (ml < 0 || second) {
+          bad = kWalkFallback;
+        } else if (S < ml) {
+          const uint32_t span = (uint32_t)(min(L, ml) - S);
+          uint64_t dd;
+          if (!walk_xlate(R, nreg, data + (uint64_t)S, span, &dd)) {
+            bad = kWalkUnmapped;
+          } else {
+            int r = 0;  // the region (walk_xlate's search, for its index)
+            for (int lo_i = 0, hi_i = nreg; lo_i < hi_i;) {
+              const int mid = (lo_i + hi_i) >> 1;
+              if (R[mid].base <= data + (uint64_t)S) {
+                lo_i = mid + 1;
+                r = mid;
+              } else {
+                hi_i = mid;
+              }
+            }
+            off = dd;
+            len = span;
+            lo = dd;
+            hi = dd + span;
+            bytes = span;
+            rmin = rmax = (uint32_t)r;
+          }
+        }
+      }
+    }
+    off_out[i] = off;
+    len_out[i] = len;
+    if (seed_out) seed_out[i] = jseed ? jseed[i] : 0u;
+  }
+  for (int d = 32; d; d >>= 1) {
+    const uint64_t olo = (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)lo, d) |
+                         (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(lo >> 32), d) << 32;
+    const uint64_t ohi = (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)hi, d) |
+                         (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(hi >> 32), d) << 32;
+    const uint64_t ob = (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)bytes, d) |
+                        (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(bytes >> 32), d) << 32;
+    lo = min(lo, olo);
+    hi = max(hi, ohi);
+    bytes += ob;
+    bad |= (uint32_t)__shfl_xor((int)bad, d);
+    rmin = min(rmin, (uint32_t)__shfl_xor((int)rmin, d));
+    rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, d));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (bytes) {
+      atomicMin(&stats[0], (unsigned long long)lo);
+      atomicMax(&stats[1], (unsigned long long)hi);
+      atomicAdd(&stats[2], (unsigned long long)bytes);
+      atomicMin(&stats[4], (unsigned long long)rmin);
+      atomicMax(&stats[5], (unsigned long long)rmax);
+    }
+    if (bad) atomicOr(&stats[3], (unsigned long long)bad);
+  }
+}
+
+// off[i] := its offset from gbase (0 for an empty span: the span kernel may
+// read its base, which the caller keeps readable).
+__global__ __launch_bounds__(256) void k_span_rebase(uint64_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ len, uint32_t n,
+                                                     uint64_t gbase) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) off[i] = len[i] ? off[i] - gbase : 0ull;
+}
+
 }  // namespace
+
+int launch_span_walk(const uint64_t* heads, const int32_t* len, const int32_t* skip,
+                     const uint32_t* seed, const WalkRegionHost* regions, int nreg, uint32_t n,
+                     bool pseudo, uint64_t* off_out, uint32_t* len_out, uint32_t* seed_out,
+                     unsigned long long* stats, hipStream_t stream) {
+  if (n == 0) return UINET_CKSUM_OK;
+  if (nreg < 1 || nreg > kWalkRegionsMax) return UINET_CKSUM_EINVAL;
+  UINET_LAUNCH(k_span_walk, dim3((n + 255) / 256), dim3(256), 0, stream, heads, len, skip, seed,
+               regions, nreg, n, pseudo ? 1 : 0, off_out, len_out, seed_out, stats);
+  return check_launch();
+}
+
+int launch_span_rebase(uint64_t* off, const uint32_t* len, uint32_t n, uint64_t gbase,
+                       hipStream_t stream) {
+  if (n == 0) return UINET_CKSUM_OK;
+  UINET_LAUNCH(k_span_rebase, dim3((n + 255) / 256), dim3(256), 0, stream, off, len, n, gbase);
+  return check_launch();
+}
 
 int launch_walk_mbufs(const uint64_t* heads, const int32_t* len, const int32_t* skip,
                       const uint32_t* seed, const WalkRegionHost* regions, int nreg, uint32_t n,

@@ -15,6 +15,8 @@ Engine paths per workload:
               (nothing registered)
   zero_copy   the packet bytes are registered; the host walks the chains and
               writes descriptors, the GPU reads the bytes in place over PCIe
+  span_gpu    bytes AND mbufs registered, one mbuf per packet: the span path
+              with the head mbufs read by the GPU (k_span_walk)
   dev_walk    bytes AND mbufs registered; the GPU walks the chains and folds
               their bytes in one launch (csrc/cksum_mbufs.hip, knob walk_device
               3) -- the host only writes the jobs
@@ -104,6 +106,7 @@ PATHS = ("staged", "zero_copy", "dev_walk")
 def run_paths(name, n, nbytes, fn, bytes_bufs, mbuf_bufs, threads, reps, check, res):
     """Every engine path x host_threads for one workload; check(out) -> bool."""
     paths = (("staged", []), ("zero_copy", bytes_bufs), ("span", bytes_bufs),
+             ("span_gpu", bytes_bufs + mbuf_bufs),
              ("dev_walk", bytes_bufs + mbuf_bufs), ("dev_walk2", bytes_bufs + mbuf_bufs))
     for path, bufs in paths:
         if path not in PATHS:
@@ -115,7 +118,7 @@ def run_paths(name, n, nbytes, fn, bytes_bufs, mbuf_bufs, threads, reps, check, 
             u.set_tuning("walk_device", 2 if path == "dev_walk2" else 3)
             # span: the single-mbuf span path (only one-mbuf sums take it);
             # the other paths with it off
-            u.set_tuning("span_fast", 1 if path == "span" else 0)
+            u.set_tuning("span_fast", 1 if path in ("span", "span_gpu") else 0)
             with Regs(bufs):
                 fn()  # warm: staging buffers, pool threads, walk row size
                 e, out = meter(fn, reps)

@@ -174,7 +174,7 @@ def test_set_tuning_validation():
           ("chains_long", 16), ("xcd_remap", 0), ("host_threads", 64), ("multi_gather", 1),
           ("walk_device", 0), ("walk_device", 1), ("walk_device", 2), ("walk_device", 3),
           ("chains_wide", 2),
-          ("span_fast", 0), ("span_fast", 1)]
+          ("span_fast", 0), ("span_fast", 1), ("span_fast", 2)]
     # chains_variant, spans_lut, spans_contig and spans_pipe 2 (k_spans_pp)
     # were removed in round 3; spans_sdesc, host_group and walk_prefetch 2 in
     # round 4; spans_pipe, spans_geo, chains_pass, chains_tile, host_pin and
@@ -184,7 +184,7 @@ def test_set_tuning_validation():
            ("chains_variant", 0), ("spans_lut", 1), ("spans_contig", 0), ("walk_device", 4),
            ("walk_device", -1), ("chains_wide", 3), ("spans_pipe", 1), ("spans_geo", 0),
            ("chains_pass", 2), ("chains_tile", 0), ("host_pin", 0), ("walk_prefetch", 1),
-           ("span_fast", 2), ("no_such_knob", 1)]
+           ("span_fast", 3), ("no_such_knob", 1)]
     try:
         for k, v in ok:
             assert L.uinet_cksum_set_tuning(k.encode(), v) == 0, (k, v)

@@ -143,7 +143,7 @@ def _host_trial(ora, arena, t):
     rng = np.random.default_rng(70000 + BASE + t)
     u.set_tuning("host_threads", int(rng.choice([1, 2, 5, 16])))
     u.set_tuning("walk_device", int(rng.integers(0, 4)))
-    u.set_tuning("span_fast", int(rng.random() < 0.8))
+    u.set_tuning("span_fast", int(rng.choice([0, 1, 1, 2, 2])))
     n = int(rng.choice([1, 7, 64, 200, int(rng.integers(1, 2500))]))
     nseg = rng.integers(1, int(rng.choice([2, 6, 30])) + 1, n)  # a chain is >= 1 mbuf
     if rng.random() < 0.3:  # one mbuf per packet: the single-mbuf span path's shape

@@ -31,6 +31,16 @@ def registered(*bufs):
             u.unregister_host(b)
 
 
+@pytest.fixture(autouse=True, params=[1, 2], ids=["host-heads", "gpu-heads"])
+def span_mode(request):
+    """Every test under both span forms: the calling thread reads the head
+    mbufs (span_fast 1), or -- where the mbufs are registered -- the GPU does
+    (span_fast 2, k_span_walk; with only the bytes registered it is form 1)."""
+    u.set_tuning("span_fast", request.param)
+    yield request.param
+    u.set_tuning("span_fast", 1)
+
+
 def spans(fn):
     """(result, span batches during fn())."""
     before = u.host_cpu()["span_batches"]
@@ -50,7 +60,7 @@ def _one_mbuf(rng, arena, n, max_len=3000):
 
 
 @pytest.mark.parametrize("mbufs_registered", [False, True])
-def test_span_path_skip_batch(ora, arena, mbufs_registered):
+def test_span_path_skip_batch(ora, arena, mbufs_registered, span_mode):
     """One mbuf per packet at random offsets (odd addresses included), len
     short of / equal to / beyond the mbuf, skip inside / at / past its end,
     len <= skip, empty mbufs; with only the bytes or also the mbufs
@@ -67,9 +77,13 @@ def test_span_path_skip_batch(ora, arena, mbufs_registered):
     skip = np.where(rng.random(n) < 0.05, ln + 7, skip)       # skip past the only mbuf
     want = ora.skip_batch(ch.heads, length, skip)
     bufs = (arena, ch.mbufs) if mbufs_registered else (arena,)
+    w0 = u.host_cpu()["device_walks"]
     with registered(*bufs):
         got, ns = spans(lambda: u.in_cksum_skip_batch(ch.heads, length, skip))
     assert ns == 1
+    # the GPU read the heads exactly when asked to and able to
+    gpu_read = u.host_cpu()["device_walks"] - w0
+    assert gpu_read == (1 if (span_mode == 2 and mbufs_registered) else 0)
     np.testing.assert_array_equal(got, want)
 
 

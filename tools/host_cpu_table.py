@@ -16,7 +16,7 @@ WORK = (("c2", "host-mbuf batch, config 2 (1,048,576 x 1500 B, one mbuf each)"),
         ("tx_hook", "TX offload hook, 65,536 mixed frames"),
         ("rx_hook", "RX offload hook, 65,536 mixed frames"),
         ("echo", "config 1, echo TX + RX call sequence, 65,536 segments"))
-PATHS = ("staged", "zero_copy", "span", "dev_walk", "dev_walk2")
+PATHS = ("staged", "zero_copy", "span", "span_gpu", "dev_walk", "dev_walk2")
 
 
 def load(path):
