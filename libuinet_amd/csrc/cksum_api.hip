@@ -979,15 +979,10 @@ __attribute__((noinline)) int span_run(HeadFn head, JobFn job, int i, const int 
   const uintptr_t hb = R.hb, lo = R.lo, hi = R.hi;
   uint64_t add = 0;
   uintptr_t top = 0;
-  const int pf_end = e - kSpanPrefetch;
-  for (; i < e; i++) {
-    if (i < pf_end) {
-      const auto r = head(i + kSpanPrefetch);
-      if (r.m) __builtin_prefetch(r.m, 0, 3);
-    }
-    const Job J = job(i);
+  const auto one = [&](int k) -> bool {
+    const Job J = job(k);
     const MbufHdr* m = J.m;
-    if (!m) break;
+    if (!m) return false;
     const long ml = m->m_len, S = J.skip, L = J.len;
     const uintptr_t a = reinterpret_cast<uintptr_t>(m->m_data) + (uintptr_t)S;
     const long span = std::min(L, ml) - S;
@@ -995,13 +990,23 @@ __attribute__((noinline)) int span_run(HeadFn head, JobFn job, int i, const int 
     // (in_cksum.c:203-229), a packed length, inside [lo, hi)
     const bool ok = (S >= 0) & (S < ml) & (L > S) & ((L <= ml) | (m->m_next == nullptr)) &
                     (span <= 0xffffL) & (a >= lo) & (a + (uintptr_t)span <= hi);
-    if (!ok) break;
-    so[i] = (uint32_t)(a - hb);
-    sl[i] = (uint16_t)span;
-    if (sd) sd[i] = J.seed;
+    if (!ok) return false;
+    so[k] = (uint32_t)(a - hb);
+    sl[k] = (uint16_t)span;
+    if (sd) sd[k] = J.seed;
     add += (uint64_t)span;
     top = std::max(top, a + (uintptr_t)span);
+    return true;
+  };
+  // (a prefetch of a null head is dropped by the core: no test)
+  const int e1 = std::max(i, e - kSpanPrefetch);
+  for (; i < e1; i++) {
+    __builtin_prefetch(head(i + kSpanPrefetch).m, 0, 3);
+    if (!one(i)) break;
   }
+  if (i >= e1)
+    for (; i < e; i++)
+      if (!one(i)) break;
   R.add = add;
   R.top = top;
   return i;
