@@ -249,3 +249,35 @@ def test_span_path_dense_pseudo_header(ora):
                                                                 proto))
     assert ns == 1 and u.host_cpu()["span_dma_bytes"] > before
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("first", ["a", "b"])
+def test_span_path_two_regions_interleaved(ora, arena, first):
+    """Packets from two registered regions, in runs and then alternating at
+    random: the common-packet run (span_run) holds one region's bounds, so a
+    packet from the other leaves it for the general code (above the group's
+    origin: offsets from it across regions; below: the group's offsets move
+    to the batch's base) and the next one re-enters it.  Either region first.
+    Edge packets (empty sums, skip at and past the mbuf's end) among them."""
+    rng = np.random.default_rng(23 if first == "a" else 24)
+    other = rand_arena(4 << 20, 25)
+    n = 30000
+    src = np.zeros(n, bool)
+    src[1000:2000] = True
+    src[2000:] = rng.random(n - 2000) < 0.3
+    if first == "b":
+        src = ~src
+    ln = rng.integers(0, 1501, n)
+    offs = np.where(src, rng.integers(0, other.size - 1502, n), rng.integers(0, arena.size - 1502, n))
+    ch_a = MbufChains.contiguous(arena, offs, ln)
+    ch_b = MbufChains.contiguous(other, offs, ln)
+    heads = np.where(src, ch_b.heads, ch_a.heads)
+    skip = np.where(rng.random(n) < 0.5, rng.integers(0, 60, n), 0)
+    skip = np.where(rng.random(n) < 0.02, ln, skip)
+    skip = np.where(rng.random(n) < 0.02, ln + 3, skip)
+    length = np.where(rng.random(n) < 0.1, rng.integers(0, ln + 1), ln)
+    want = ora.skip_batch(heads, length, skip)
+    with registered(arena, other):
+        got, ns = spans(lambda: u.in_cksum_skip_batch(heads, length, skip))
+    assert ns == 1
+    np.testing.assert_array_equal(got, want)
