@@ -138,6 +138,7 @@ def main():
     ap.add_argument("--threads", default="1,16")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--c2-packets", type=int, default=1 << 20)
+    ap.add_argument("--c3-packets", type=int, default=1 << 18)
     ap.add_argument("--paths", default="staged,zero_copy,dev_walk")
     a = ap.parse_args()
     global PATHS
@@ -163,7 +164,7 @@ def main():
                   [arena], [ch.mbufs], threads, a.reps, lambda o: np.array_equal(o, want), res)
         del arena, ch
     if "c3" in work:
-        c3 = build_config3(1 << 18, seed=3)
+        c3 = build_config3(a.c3_packets, seed=3)
         ch3 = MbufChains(c3["arena"], c3["seg_off"], c3["seg_len"], c3["pkt_seg"])
         n = ch3.n
         nb = int((c3["lens"] - 20).sum())
