@@ -219,3 +219,28 @@ def test_in6_gpu(torch_dev, v6, ora):
             u.unregister_host(ch.mbufs)
     finally:
         u.unregister_host(ch.arena)
+
+
+@pytest.mark.gpu
+def test_in6_gpu_single_mbuf_spans(torch_dev, v6, ora):
+    """The same IPv6 packets laid out one mbuf each (the RX shape) in one
+    registered arena: in6_cksum_batch takes the single-mbuf span path, each
+    packet's pseudo-header fold riding as its seed, packet after packet in
+    the common-packet run (span_run) -- bit-exact against the oracle."""
+    import libuinet_amd as u
+
+    _, nxt, off, ln, pkts = v6
+    sizes = np.array([len(p) for p in pkts], np.int64)
+    starts = 1 + np.concatenate([[0], np.cumsum(sizes)[:-1]])  # odd and even starts
+    arena = aligned_empty(int(starts[-1] + sizes[-1] + 64))
+    for s, p in zip(starts, pkts):
+        arena[s:s + len(p)] = np.frombuffer(p, np.uint8)
+    ch = MbufChains.contiguous(arena, starts, sizes)
+    want = ora.in6_cksum_batch(ch.heads, nxt, off, ln)
+    u.register_host(arena)
+    try:
+        s0 = u.host_cpu()["span_batches"]
+        np.testing.assert_array_equal(u.in6_cksum_batch(ch.heads, nxt, off, ln), want)
+        assert u.host_cpu()["span_batches"] == s0 + 1
+    finally:
+        u.unregister_host(arena)

@@ -281,3 +281,27 @@ def test_span_path_two_regions_interleaved(ora, arena, first):
         got, ns = spans(lambda: u.in_cksum_skip_batch(heads, length, skip))
     assert ns == 1
     np.testing.assert_array_equal(got, want)
+
+
+def test_span_path_two_regions_pseudo_header(ora, arena):
+    """The pseudo-header form (seeds in the common-packet run) over packets
+    from two registered regions, alternating in runs of random length."""
+    rng = np.random.default_rng(26)
+    other = rand_arena(4 << 20, 27)
+    n = 20000
+    src = np.repeat(rng.random(200) < 0.5, 100)
+    ln = rng.integers(0, 1501, n)
+    offs = np.where(src, rng.integers(0, other.size - 1502, n), rng.integers(0, arena.size - 1502, n))
+    ch_a = MbufChains.contiguous(arena, offs, ln)
+    ch_b = MbufChains.contiguous(other, offs, ln)
+    heads = np.where(src, ch_b.heads, ch_a.heads)
+    off0 = np.minimum(ln, rng.integers(0, 41, n))
+    plen = np.maximum(0, ln - off0 - rng.integers(0, 30, n))
+    s_ip, d_ip = (rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) for _ in range(2))
+    proto = rng.choice(np.array([6, 17], np.uint8), n)
+    want = ora.pseudo_header_batch(heads, plen, off0, s_ip, d_ip, proto)
+    with registered(arena, other):
+        got, ns = spans(lambda: u.in_cksum_pseudo_header_batch(heads, plen, off0, s_ip, d_ip,
+                                                                proto))
+    assert ns == 1
+    np.testing.assert_array_equal(got, want)
